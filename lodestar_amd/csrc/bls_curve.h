@@ -1,0 +1,431 @@
+// G1 / G2 group arithmetic on CDNA4, one point per lane.
+//
+// E1: y^2 = x^3 + 4 over Fp;  E2: y^2 = x^3 + 4(1+i) over Fp2.
+// Points are Jacobian (X, Y, Z), x = X/Z^2, y = Y/Z^3, infinity <=> Z == 0.
+// Formulas: dbl-2009-l, add-2007-bl, madd-2007-bl (a = 0), made complete with
+// rare-case branches (equal inputs -> double, infinity operands).
+#pragma once
+#include "bls_field.h"
+
+// ---------------------------------------------------------------------------
+// overload set so the point code is written once for Fp and Fp2
+// ---------------------------------------------------------------------------
+BGV_HD fp_t f_add(const fp_t& a, const fp_t& b) { return fp_add(a, b); }
+BGV_HD fp_t f_sub(const fp_t& a, const fp_t& b) { return fp_sub(a, b); }
+BGV_HD fp_t f_dbl(const fp_t& a) { return fp_dbl(a); }
+BGV_HD fp_t f_neg(const fp_t& a) { return fp_neg(a); }
+BGV_HD fp_t f_mul(const fp_t& a, const fp_t& b) { return fp_mul(a, b); }
+BGV_HD fp_t f_sqr(const fp_t& a) { return fp_sqr(a); }
+BGV_HD bool f_is_zero(const fp_t& a) { return fp_is_zero(a); }
+BGV_HD bool f_eq(const fp_t& a, const fp_t& b) { return fp_eq(a, b); }
+BGV_HD fp_t f_select(bool c, const fp_t& a, const fp_t& b) { return fp_select(c, a, b); }
+BGV_HD fp_t f_inv(const fp_t& a) { return fp_inv(a); }
+BGV_HD void f_set_zero(fp_t* a) { *a = fp_zero(); }
+BGV_HD void f_set_one(fp_t* a) { *a = fp_one(); }
+
+BGV_HD fp2_t f_add(const fp2_t& a, const fp2_t& b) { return fp2_add(a, b); }
+BGV_HD fp2_t f_sub(const fp2_t& a, const fp2_t& b) { return fp2_sub(a, b); }
+BGV_HD fp2_t f_dbl(const fp2_t& a) { return fp2_dbl(a); }
+BGV_HD fp2_t f_neg(const fp2_t& a) { return fp2_neg(a); }
+BGV_HD fp2_t f_mul(const fp2_t& a, const fp2_t& b) { return fp2_mul(a, b); }
+BGV_HD fp2_t f_sqr(const fp2_t& a) { return fp2_sqr(a); }
+BGV_HD bool f_is_zero(const fp2_t& a) { return fp2_is_zero(a); }
+BGV_HD bool f_eq(const fp2_t& a, const fp2_t& b) { return fp2_eq(a, b); }
+BGV_HD fp2_t f_select(bool c, const fp2_t& a, const fp2_t& b) { return fp2_select(c, a, b); }
+BGV_HD fp2_t f_inv(const fp2_t& a) { return fp2_inv(a); }
+BGV_HD void f_set_zero(fp2_t* a) { *a = fp2_zero(); }
+BGV_HD void f_set_one(fp2_t* a) { *a = fp2_one(); }
+
+template <class F>
+struct jac_t {
+  F x, y, z;
+};
+template <class F>
+struct aff_t {
+  F x, y;
+};
+
+typedef jac_t<fp_t> g1_jac;
+typedef aff_t<fp_t> g1_aff;
+typedef jac_t<fp2_t> g2_jac;
+typedef aff_t<fp2_t> g2_aff;
+
+template <class F>
+BGV_HD jac_t<F> jac_infinity() {
+  jac_t<F> r;
+  f_set_one(&r.x);
+  f_set_one(&r.y);
+  f_set_zero(&r.z);
+  return r;
+}
+
+template <class F>
+BGV_HD bool jac_is_inf(const jac_t<F>& p) {
+  return f_is_zero(p.z);
+}
+
+template <class F>
+BGV_HD jac_t<F> jac_from_aff(const aff_t<F>& a) {
+  jac_t<F> r;
+  r.x = a.x;
+  r.y = a.y;
+  f_set_one(&r.z);
+  return r;
+}
+
+template <class F>
+BGV_HD jac_t<F> jac_select(bool c, const jac_t<F>& a, const jac_t<F>& b) {
+  return jac_t<F>{f_select(c, a.x, b.x), f_select(c, a.y, b.y), f_select(c, a.z, b.z)};
+}
+
+template <class F>
+BGV_HD jac_t<F> jac_neg(const jac_t<F>& p) {
+  return jac_t<F>{p.x, f_neg(p.y), p.z};
+}
+
+// dbl-2009-l
+template <class F>
+BGV_HD jac_t<F> jac_dbl(const jac_t<F>& p) {
+  F A = f_sqr(p.x);
+  F B = f_sqr(p.y);
+  F C = f_sqr(B);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
+  F E = f_add(f_dbl(A), A);
+  F Fq = f_sqr(E);
+  jac_t<F> r;
+  r.x = f_sub(Fq, f_dbl(D));
+  F C8 = f_dbl(f_dbl(f_dbl(C)));
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
+  r.z = f_dbl(f_mul(p.y, p.z));
+  return r;
+}
+
+// add-2007-bl with the generic-case formulas; flags equal/opposite inputs.
+template <class F>
+BGV_HD jac_t<F> jac_add_raw(const jac_t<F>& p, const jac_t<F>& q, bool* h_zero, bool* r_zero) {
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, U1);
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F rr = f_dbl(f_sub(S2, S1));
+  F V = f_mul(U1, I);
+  jac_t<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
+  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  *h_zero = f_is_zero(H);
+  *r_zero = f_is_zero(rr);
+  return r;
+}
+
+// complete addition
+template <class F>
+BGV_HD jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
+  bool hz, rz;
+  jac_t<F> r = jac_add_raw(p, q, &hz, &rz);
+  const bool pinf = jac_is_inf(p), qinf = jac_is_inf(q);
+  if (hz && rz && !pinf && !qinf) r = jac_dbl(p);  // rare: P == Q
+  r = jac_select(pinf, r, q);
+  r = jac_select(qinf && !pinf, r, p);
+  return r;
+}
+
+// madd-2007-bl: p Jacobian + q affine (q never infinity)
+template <class F>
+BGV_HD jac_t<F> jac_add_aff_raw(const jac_t<F>& p, const aff_t<F>& q, bool* h_zero, bool* r_zero) {
+  F Z1Z1 = f_sqr(p.z);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S2 = f_mul(q.y, f_mul(p.z, Z1Z1));
+  F H = f_sub(U2, p.x);
+  F HH = f_sqr(H);
+  F I = f_dbl(f_dbl(HH));
+  F J = f_mul(H, I);
+  F rr = f_dbl(f_sub(S2, p.y));
+  F V = f_mul(p.x, I);
+  jac_t<F> r;
+  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
+  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
+  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  *h_zero = f_is_zero(H);
+  *r_zero = f_is_zero(rr);
+  return r;
+}
+
+template <class F>
+BGV_HD jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
+  bool hz, rz;
+  jac_t<F> r = jac_add_aff_raw(p, q, &hz, &rz);
+  const bool pinf = jac_is_inf(p);
+  if (hz && rz && !pinf) r = jac_dbl(p);
+  r = jac_select(pinf, r, jac_from_aff(q));
+  return r;
+}
+
+// Jacobian -> affine; returns false for infinity (out untouched = zeros).
+template <class F>
+BGV_HD bool jac_to_aff(aff_t<F>* out, const jac_t<F>& p) {
+  F zi = f_inv(p.z);
+  F zi2 = f_sqr(zi);
+  out->x = f_mul(p.x, zi2);
+  out->y = f_mul(p.y, f_mul(zi2, zi));
+  return !jac_is_inf(p);
+}
+
+template <class F>
+BGV_HD bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
+  const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  F Z1Z1 = f_sqr(p.z), Z2Z2 = f_sqr(q.z);
+  bool ex = f_eq(f_mul(p.x, Z2Z2), f_mul(q.x, Z1Z1));
+  bool ey = f_eq(f_mul(f_mul(p.y, q.z), Z2Z2), f_mul(f_mul(q.y, p.z), Z1Z1));
+  return (pi && qi) || (!pi && !qi && ex && ey);
+}
+
+// [k]P for a 64-bit (lane-varying) scalar: left-to-right, 2-bit fixed window
+// with a 3-entry table; the add is computed in every lane and selected, so a
+// wave never diverges on scalar bits.
+template <class F>
+BGV_HD jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
+  jac_t<F> t1 = p;
+  jac_t<F> t2 = jac_dbl(p);
+  jac_t<F> t3 = jac_add(t2, p);
+  jac_t<F> acc = jac_infinity<F>();
+  BGV_NO_UNROLL for (int i = 62; i >= 0; i -= 2) {
+    acc = jac_dbl(jac_dbl(acc));
+    const uint32_t d = (uint32_t)(k >> i) & 3u;
+    jac_t<F> s = jac_select(d == 2u, t1, t2);
+    s = jac_select(d == 3u, s, t3);
+    jac_t<F> sum = jac_add(acc, s);
+    acc = jac_select(d != 0u, acc, sum);
+  }
+  return acc;
+}
+
+// [|x|]P, |x| = 0xd201000000010000 (lane-uniform bits: no divergence)
+template <class F>
+BGV_HD jac_t<F> jac_mul_x_abs(const jac_t<F>& p) {
+  jac_t<F> acc = p;
+  const uint64_t X = BGV_X_ABS;
+  BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl(acc);
+    if ((X >> i) & 1) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// G1 helpers
+// ---------------------------------------------------------------------------
+BGV_HD g1_aff g1_generator() {
+  g1_aff g;
+  g.x = fp_t{BGV_G1X};
+  g.y = fp_t{BGV_G1Y};
+  return g;
+}
+
+BGV_HD g1_aff g1_neg_generator() {
+  g1_aff g;
+  g.x = fp_t{BGV_G1X};
+  g.y = fp_t{BGV_NEG_G1Y};
+  return g;
+}
+
+BGV_HD bool g1_aff_on_curve(const g1_aff& a) {
+  const fp_t b = {BGV_B1};
+  return fp_eq(fp_sqr(a.y), fp_add(fp_mul(fp_sqr(a.x), a.x), b));
+}
+
+// ---------------------------------------------------------------------------
+// G2 helpers: psi endomorphism and subgroup check
+// ---------------------------------------------------------------------------
+BGV_HD g2_jac g2_psi(const g2_jac& p) {
+  const fp2_t cx = BGV_PSI_CX;
+  const fp2_t cy = BGV_PSI_CY;
+  g2_jac r;
+  r.x = fp2_mul(fp2_conj(p.x), cx);
+  r.y = fp2_mul(fp2_conj(p.y), cy);
+  r.z = fp2_conj(p.z);
+  return r;
+}
+
+BGV_HD g2_jac g2_psi2(const g2_jac& p) {
+  const fp_t cx = {BGV_PSI2_CX};
+  const fp_t cy = {BGV_PSI2_CY};
+  g2_jac r;
+  r.x = fp2_mul_fp(p.x, cx);
+  r.y = fp2_mul_fp(p.y, cy);
+  r.z = p.z;
+  return r;
+}
+
+BGV_HD bool g2_aff_on_curve(const g2_aff& a) {
+  const fp2_t b = BGV_B2;
+  return fp2_eq(fp2_sqr(a.y), fp2_add(fp2_mul(fp2_sqr(a.x), a.x), b));
+}
+
+// P in G2  <=>  psi(P) == [x]P == -[|x|]P   (Scott, "A note on group membership
+// tests for G1, G2 and GT on BLS pairing-friendly curves"; blst POINTonE2_in_G2)
+BGV_HD bool g2_in_subgroup(const g2_jac& p) {
+  g2_jac q = jac_neg(jac_mul_x_abs(p));
+  return jac_eq(g2_psi(p), q);
+}
+
+// [x]P with x = -|x|
+template <class F>
+BGV_HD jac_t<F> jac_mul_x(const jac_t<F>& p) {
+  return jac_neg(jac_mul_x_abs(p));
+}
+
+// RFC 9380 G.4 clear_cofactor: (x^2 - x - 1)P + (x - 1)psi(P) + 2 psi^2(P)
+BGV_HD g2_jac g2_clear_cofactor(const g2_jac& p) {
+  g2_jac t1 = jac_mul_x(p);
+  g2_jac t2 = g2_psi(p);
+  g2_jac t3 = g2_psi2(jac_dbl(p));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = jac_mul_x(t2);
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(p));
+}
+
+// ---------------------------------------------------------------------------
+// ZCash serialisation (big-endian; flags in the top 3 bits of byte 0)
+// ---------------------------------------------------------------------------
+enum {
+  BGV_OK = 0,
+  BGV_BAD_ENCODING = 1,
+  BGV_POINT_NOT_ON_CURVE = 2,
+  BGV_POINT_NOT_IN_GROUP = 3,
+  BGV_PK_IS_INFINITY = 6,
+  BGV_INVALID_SIZE = 8,
+};
+
+// 96-byte compressed G2 (signature) -> affine; *inf set for the infinity
+// encoding.  Mirrors blst_p2_uncompress; returns a BGV_* code.
+BGV_HD int g2_decompress(g2_aff* out, bool* inf, const uint8_t* b) {
+  const uint8_t flags = b[0];
+  *inf = false;
+  if (!(flags & 0x80)) return BGV_BAD_ENCODING;
+  if (flags & 0x40) {
+    uint8_t acc = flags & 0x3f;
+    for (int i = 1; i < 96; ++i) acc |= b[i];
+    if (acc) return BGV_BAD_ENCODING;
+    *inf = true;
+    return BGV_OK;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  fp_t x1 = fp_from_be48(tmp);
+  fp_t x0 = fp_from_be48(b + 48);
+  if (!fp_raw_lt_p(x1) || !fp_raw_lt_p(x0)) return BGV_BAD_ENCODING;
+  fp2_t x = {fp_to_mont(x0), fp_to_mont(x1)};
+  const fp2_t B = BGV_B2;
+  fp2_t y2 = fp2_add(fp2_mul(fp2_sqr(x), x), B);
+  fp2_t y;
+  if (!fp2_sqrt(&y, y2)) return BGV_POINT_NOT_ON_CURVE;
+  const bool want = (flags & 0x20) != 0;
+  if (fp2_lex_largest(y) != want) y = fp2_neg(y);
+  out->x = x;
+  out->y = y;
+  return BGV_OK;
+}
+
+BGV_HD void g2_compress(uint8_t* b, const g2_aff& a, bool inf) {
+  if (inf) {
+    b[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(b, fp_from_mont(a.x.c1));
+  fp_to_be48(b + 48, fp_from_mont(a.x.c0));
+  b[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+}
+
+BGV_HD void g2_serialize(uint8_t* b, const g2_aff& a, bool inf) {
+  if (inf) {
+    b[0] = 0x40;
+    for (int i = 1; i < 192; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(b, fp_from_mont(a.x.c1));
+  fp_to_be48(b + 48, fp_from_mont(a.x.c0));
+  fp_to_be48(b + 96, fp_from_mont(a.y.c1));
+  fp_to_be48(b + 144, fp_from_mont(a.y.c0));
+}
+
+// 96-byte uncompressed G1 (trusted pubkey bytes, worker.ts:110-116): no
+// subgroup or curve check; flags only.
+BGV_HD int g1_deserialize(g1_aff* out, bool* inf, const uint8_t* b) {
+  const uint8_t flags = b[0];
+  *inf = false;
+  if (flags & 0x80) return BGV_BAD_ENCODING;
+  if (flags & 0x40) {
+    uint8_t acc = flags & 0x3f;
+    for (int i = 1; i < 96; ++i) acc |= b[i];
+    if (acc) return BGV_BAD_ENCODING;
+    *inf = true;
+    return BGV_OK;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  fp_t x = fp_from_be48(tmp);
+  fp_t y = fp_from_be48(b + 48);
+  if (!fp_raw_lt_p(x) || !fp_raw_lt_p(y)) return BGV_BAD_ENCODING;
+  out->x = fp_to_mont(x);
+  out->y = fp_to_mont(y);
+  return BGV_OK;
+}
+
+// 48-byte compressed G1 -> affine (blst_p1_uncompress)
+BGV_HD int g1_decompress(g1_aff* out, bool* inf, const uint8_t* b) {
+  const uint8_t flags = b[0];
+  *inf = false;
+  if (!(flags & 0x80)) return BGV_BAD_ENCODING;
+  if (flags & 0x40) {
+    uint8_t acc = flags & 0x3f;
+    for (int i = 1; i < 48; ++i) acc |= b[i];
+    if (acc) return BGV_BAD_ENCODING;
+    *inf = true;
+    return BGV_OK;
+  }
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  fp_t xr = fp_from_be48(tmp);
+  if (!fp_raw_lt_p(xr)) return BGV_BAD_ENCODING;
+  fp_t x = fp_to_mont(xr);
+  const fp_t B = {BGV_B1};
+  fp_t y;
+  if (!fp_sqrt(&y, fp_add(fp_mul(fp_sqr(x), x), B))) return BGV_POINT_NOT_ON_CURVE;
+  if (fp_lex_largest(y) != ((flags & 0x20) != 0)) y = fp_neg(y);
+  out->x = x;
+  out->y = y;
+  return BGV_OK;
+}
+
+BGV_HD void g1_serialize(uint8_t* b, const g1_aff& a, bool inf) {
+  if (inf) {
+    b[0] = 0x40;
+    for (int i = 1; i < 96; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(b, fp_from_mont(a.x));
+  fp_to_be48(b + 48, fp_from_mont(a.y));
+}
+
+BGV_HD void g1_compress(uint8_t* b, const g1_aff& a, bool inf) {
+  if (inf) {
+    b[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) b[i] = 0;
+    return;
+  }
+  fp_to_be48(b, fp_from_mont(a.x));
+  b[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
+}

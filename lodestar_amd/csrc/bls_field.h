@@ -1,0 +1,524 @@
+// BLS12-381 field tower for CDNA4 (gfx950): Fp, Fp2, Fp6, Fp12.
+//
+// One field element per lane: Fp = 12 x u32 limbs (little-endian) in Montgomery
+// form with R = 2^384, always fully reduced to [0, p).  Multiplication is
+// 12-limb CIOS whose inner step `(u64)a*b + t + c` lowers to v_mad_u64_u32
+// plus a 64-bit add (measured issue rate on MI355X: 16 lanes/clk/SIMD for the
+// mad, tools/ubench_valu.hip).
+//
+// Tower (same as blst / the IETF pairing draft):
+//   Fp2  = Fp[i]  / (i^2 + 1)
+//   Fp6  = Fp2[v] / (v^3 - (1 + i))
+//   Fp12 = Fp6[w] / (w^2 - v)
+//
+// The same source compiles for the host (tests/hostsim) so every formula is
+// unit-tested against oracle/bls12381.py on the CPU before it runs on a GPU.
+#pragma once
+#include <stdint.h>
+
+#include "bls_constants.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BGV_HD __host__ __device__ __forceinline__
+#define BGV_NOINLINE __host__ __device__ __noinline__
+#define BGV_CONST __constant__
+#else
+#define BGV_HD inline __attribute__((always_inline))
+#define BGV_NOINLINE __attribute__((noinline))
+#define BGV_CONST static const
+#endif
+
+#define BGV_UNROLL _Pragma("unroll")
+#define BGV_NO_UNROLL _Pragma("unroll 1")
+
+#define NL 12
+
+struct fp_t {
+  uint32_t v[NL];
+};
+struct fp2_t {
+  fp_t c0, c1;
+};
+struct fp6_t {
+  fp2_t c0, c1, c2;
+};
+struct fp12_t {
+  fp6_t c0, c1;
+};
+
+// ---------------------------------------------------------------------------
+// Fp
+// ---------------------------------------------------------------------------
+BGV_HD uint32_t p_limb(int i) {
+  // p as an immediate table; indices are compile-time constants after unrolling
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  return P_[i];
+}
+
+BGV_HD fp_t fp_zero() {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = 0;
+  return r;
+}
+
+BGV_HD fp_t fp_one() {
+  fp_t r = {BGV_ONE};
+  return r;
+}
+
+BGV_HD bool fp_is_zero(const fp_t& a) {
+  uint32_t acc = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+
+BGV_HD bool fp_eq(const fp_t& a, const fp_t& b) {
+  uint32_t acc = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// r = cond ? b : a   (branch-free select)
+BGV_HD fp_t fp_select(bool cond, const fp_t& a, const fp_t& b) {
+  fp_t r;
+  uint32_t m = 0u - (uint32_t)cond;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = (a.v[i] & ~m) | (b.v[i] & m);
+  return r;
+}
+
+// Reduce a value in [0, 2p) to [0, p).
+BGV_HD fp_t fp_reduce_once(const fp_t& a) {
+  fp_t d;
+  uint32_t borrow = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t s = (uint64_t)a.v[i] - p_limb(i) - borrow;
+    d.v[i] = (uint32_t)s;
+    borrow = (uint32_t)(s >> 63);
+  }
+  return fp_select(borrow == 0, a, d);
+}
+
+BGV_HD fp_t fp_add(const fp_t& a, const fp_t& b) {
+  fp_t r;
+  uint32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t s = (uint64_t)a.v[i] + b.v[i] + c;
+    r.v[i] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  return fp_reduce_once(r);  // a + b < 2p < 2^382: no carry out of limb 11
+}
+
+BGV_HD fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
+
+BGV_HD fp_t fp_sub(const fp_t& a, const fp_t& b) {
+  fp_t r, s;
+  uint32_t borrow = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
+    r.v[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  // if borrow: r += p
+  uint32_t m = 0u - borrow, c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t t = (uint64_t)r.v[i] + (p_limb(i) & m) + c;
+    s.v[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return s;
+}
+
+BGV_HD fp_t fp_neg(const fp_t& a) {
+  fp_t r;
+  uint32_t borrow = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t d = (uint64_t)p_limb(i) - a.v[i] - borrow;
+    r.v[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  // -0 = 0
+  return fp_select(fp_is_zero(a), r, a);
+}
+
+// Montgomery multiplication, CIOS, 12 x 32-bit.
+BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) {
+  uint32_t t[NL + 2];
+  BGV_UNROLL for (int i = 0; i < NL + 2; ++i) t[i] = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t c = 0;
+    const uint32_t ai = a.v[i];
+    BGV_UNROLL for (int j = 0; j < NL; ++j) {
+      uint64_t s = (uint64_t)ai * b.v[j] + t[j] + c;
+      t[j] = (uint32_t)s;
+      c = s >> 32;
+    }
+    uint64_t s = (uint64_t)t[NL] + c;
+    t[NL] = (uint32_t)s;
+    t[NL + 1] = (uint32_t)(s >> 32);
+    const uint32_t m = t[0] * BGV_N0;
+    s = (uint64_t)m * p_limb(0) + t[0];
+    c = s >> 32;
+    BGV_UNROLL for (int j = 1; j < NL; ++j) {
+      s = (uint64_t)m * p_limb(j) + t[j] + c;
+      t[j - 1] = (uint32_t)s;
+      c = s >> 32;
+    }
+    s = (uint64_t)t[NL] + c;
+    t[NL - 1] = (uint32_t)s;
+    t[NL] = t[NL + 1] + (uint32_t)(s >> 32);
+  }
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = t[i];
+  return fp_reduce_once(r);  // t < 2p since 4p < 2^384
+}
+
+BGV_HD fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
+
+// to / from Montgomery form (raw integers < p)
+BGV_HD fp_t fp_to_mont(const fp_t& a) {
+  const fp_t r2 = {BGV_R2};
+  return fp_mul(a, r2);
+}
+
+BGV_HD fp_t fp_from_mont(const fp_t& a) {
+  fp_t one = fp_zero();
+  one.v[0] = 1;
+  return fp_mul(a, one);
+}
+
+// a^e for a fixed (lane-uniform) exponent given as NL little-endian limbs.
+BGV_HD fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
+  fp_t r = fp_one();
+  BGV_NO_UNROLL for (int i = nbits - 1; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+BGV_HD fp_t fp_inv(const fp_t& a) {
+  const uint32_t e[NL] = BGV_EXP_P_MINUS_2;
+  return fp_pow_limbs(a, e, 381);
+}
+
+// a^((p-3)/4): for a QR, a * t = sqrt(a) and t = 1/sqrt(a).
+BGV_HD fp_t fp_pow_p_minus_3_div_4(const fp_t& a) {
+  const uint32_t e[NL] = BGV_EXP_P_MINUS_3_DIV_4;
+  return fp_pow_limbs(a, e, 379);
+}
+
+// sqrt candidate; returns true iff a is a square (then *out = a^((p+1)/4)).
+BGV_HD bool fp_sqrt(fp_t* out, const fp_t& a) {
+  const uint32_t e[NL] = BGV_EXP_P_PLUS_1_DIV_4;
+  fp_t s = fp_pow_limbs(a, e, 379);
+  *out = s;
+  return fp_eq(fp_sqr(s), a);
+}
+
+// a / 2 mod p
+BGV_HD fp_t fp_half(const fp_t& a) {
+  uint32_t m = 0u - (a.v[0] & 1);
+  fp_t t;
+  uint32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t s = (uint64_t)a.v[i] + (p_limb(i) & m) + c;
+    t.v[i] = (uint32_t)s;
+    c = (uint32_t)(s >> 32);
+  }
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL - 1; ++i) r.v[i] = (t.v[i] >> 1) | (t.v[i + 1] << 31);
+  r.v[NL - 1] = (t.v[NL - 1] >> 1) | (c << 31);
+  return r;
+}
+
+// Compare raw (non-Montgomery) integers: a > b
+BGV_HD bool fp_raw_gt(const fp_t& a, const fp_t& b) {
+  // b - a borrows iff a > b
+  uint32_t borrow = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t d = (uint64_t)b.v[i] - a.v[i] - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow != 0;
+}
+
+// raw integer < p ?
+BGV_HD bool fp_raw_lt_p(const fp_t& a) {
+  uint32_t borrow = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint64_t d = (uint64_t)a.v[i] - p_limb(i) - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow != 0;
+}
+
+// ZCash "lexicographically largest": raw(a) > (p-1)/2
+BGV_HD bool fp_lex_largest(const fp_t& a_mont) {
+  const fp_t half = {BGV_HALF_P_RAW};
+  return fp_raw_gt(fp_from_mont(a_mont), half);
+}
+
+// big-endian 48 bytes -> raw limbs
+BGV_HD fp_t fp_from_be48(const uint8_t* b) {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  return r;
+}
+
+BGV_HD void fp_to_be48(uint8_t* b, const fp_t& raw) {
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(raw.v[i] >> 24);
+    q[1] = (uint8_t)(raw.v[i] >> 16);
+    q[2] = (uint8_t)(raw.v[i] >> 8);
+    q[3] = (uint8_t)raw.v[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fp2
+// ---------------------------------------------------------------------------
+BGV_HD fp2_t fp2_zero() { return fp2_t{fp_zero(), fp_zero()}; }
+BGV_HD fp2_t fp2_one() { return fp2_t{fp_one(), fp_zero()}; }
+BGV_HD bool fp2_is_zero(const fp2_t& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BGV_HD bool fp2_eq(const fp2_t& a, const fp2_t& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BGV_HD fp2_t fp2_select(bool c, const fp2_t& a, const fp2_t& b) {
+  return fp2_t{fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)};
+}
+BGV_HD fp2_t fp2_add(const fp2_t& a, const fp2_t& b) { return fp2_t{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+BGV_HD fp2_t fp2_sub(const fp2_t& a, const fp2_t& b) { return fp2_t{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+BGV_HD fp2_t fp2_dbl(const fp2_t& a) { return fp2_t{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+BGV_HD fp2_t fp2_neg(const fp2_t& a) { return fp2_t{fp_neg(a.c0), fp_neg(a.c1)}; }
+BGV_HD fp2_t fp2_conj(const fp2_t& a) { return fp2_t{a.c0, fp_neg(a.c1)}; }
+
+BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+  fp_t t0 = fp_mul(a.c0, b.c0);
+  fp_t t1 = fp_mul(a.c1, b.c1);
+  fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return fp2_t{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+BGV_HD fp2_t fp2_sqr(const fp2_t& a) {
+  fp_t t = fp_mul(a.c0, a.c1);
+  return fp2_t{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+}
+
+BGV_HD fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { return fp2_t{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+
+// multiply by xi = 1 + i
+BGV_HD fp2_t fp2_mul_xi(const fp2_t& a) { return fp2_t{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+BGV_HD fp2_t fp2_inv(const fp2_t& a) {
+  fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp_t ni = fp_inv(n);
+  return fp2_t{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+BGV_HD fp2_t fp2_half(const fp2_t& a) { return fp2_t{fp_half(a.c0), fp_half(a.c1)}; }
+
+// Square root in Fp2 (p = 3 mod 4) by the norm ("complex") method with one
+// shared exponentiation for sqrt and inverse.  Returns false if a is not a
+// square.  Any root is returned; callers fix the sign.
+BGV_HD bool fp2_sqrt(fp2_t* out, const fp2_t& a) {
+  const fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp_t g;
+  const bool n_sq = fp_sqrt(&g, n);
+  const bool a1z = fp_is_zero(a.c1);
+  // delta = a1 == 0 ? a0 : (a0 + g) / 2
+  fp_t d = fp_select(a1z, fp_half(fp_add(a.c0, g)), a.c0);
+  fp_t t = fp_pow_p_minus_3_div_4(d);
+  fp_t dt = fp_mul(d, t);
+  fp_t s = fp_mul(dt, t);  // d^((p-1)/2)
+  fp_t a1t2 = fp_half(fp_mul(a.c1, t));
+  // s == 1: (d t, a1 t / 2);  s == -1: (a1 t / 2, -d t)
+  const bool qr = fp_eq(s, fp_one());
+  fp2_t y;
+  y.c0 = fp_select(qr, a1t2, dt);
+  y.c1 = fp_select(qr, fp_neg(dt), a1t2);
+  *out = y;
+  return n_sq && fp2_eq(fp2_sqr(y), a);
+}
+
+// RFC 9380 sgn0 for Fp2 (on raw values)
+BGV_HD uint32_t fp2_sgn0(const fp2_t& a_mont) {
+  fp_t a0 = fp_from_mont(a_mont.c0), a1 = fp_from_mont(a_mont.c1);
+  uint32_t s0 = a0.v[0] & 1, s1 = a1.v[0] & 1;
+  uint32_t z0 = fp_is_zero(a0) ? 1u : 0u;
+  return s0 | (z0 & s1);
+}
+
+// ZCash sign for Fp2: c1 > (p-1)/2, or c1 == 0 and c0 > (p-1)/2
+BGV_HD bool fp2_lex_largest(const fp2_t& a) {
+  const bool c1z = fp_is_zero(a.c1);
+  return c1z ? fp_lex_largest(a.c0) : fp_lex_largest(a.c1);
+}
+
+// ---------------------------------------------------------------------------
+// Fp6
+// ---------------------------------------------------------------------------
+BGV_HD fp6_t fp6_zero() { return fp6_t{fp2_zero(), fp2_zero(), fp2_zero()}; }
+BGV_HD fp6_t fp6_one() { return fp6_t{fp2_one(), fp2_zero(), fp2_zero()}; }
+BGV_HD fp6_t fp6_add(const fp6_t& a, const fp6_t& b) {
+  return fp6_t{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)};
+}
+BGV_HD fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) {
+  return fp6_t{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)};
+}
+BGV_HD fp6_t fp6_neg(const fp6_t& a) { return fp6_t{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+BGV_HD fp6_t fp6_mul_v(const fp6_t& a) { return fp6_t{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+BGV_HD fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
+  fp2_t t0 = fp2_mul(a.c0, b.c0);
+  fp2_t t1 = fp2_mul(a.c1, b.c1);
+  fp2_t t2 = fp2_mul(a.c2, b.c2);
+  fp2_t c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
+  fp2_t c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
+  fp2_t c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  return fp6_t{c0, c1, c2};
+}
+
+BGV_HD fp6_t fp6_sqr(const fp6_t& a) {
+  // CH-SQR2
+  fp2_t s0 = fp2_sqr(a.c0);
+  fp2_t ab = fp2_mul(a.c0, a.c1);
+  fp2_t s1 = fp2_dbl(ab);
+  fp2_t s2 = fp2_sqr(fp2_add(fp2_sub(a.c0, a.c1), a.c2));
+  fp2_t bc = fp2_mul(a.c1, a.c2);
+  fp2_t s3 = fp2_dbl(bc);
+  fp2_t s4 = fp2_sqr(a.c2);
+  fp2_t c0 = fp2_add(fp2_mul_xi(s3), s0);
+  fp2_t c1 = fp2_add(fp2_mul_xi(s4), s1);
+  fp2_t c2 = fp2_sub(fp2_sub(fp2_add(fp2_add(s1, s2), s3), s0), s4);
+  return fp6_t{c0, c1, c2};
+}
+
+// a * (b0 + b1 v)
+BGV_HD fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
+  fp2_t t0 = fp2_mul(a.c0, b0);
+  fp2_t t1 = fp2_mul(a.c1, b1);
+  fp2_t c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), t0);
+  fp2_t c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  fp2_t c2 = fp2_add(fp2_mul(a.c2, b0), t1);
+  return fp6_t{c0, c1, c2};
+}
+
+// a * (b1 v)
+BGV_HD fp6_t fp6_mul_1(const fp6_t& a, const fp2_t& b1) {
+  return fp6_t{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+BGV_HD fp6_t fp6_inv(const fp6_t& a) {
+  fp2_t t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  fp2_t t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  fp2_t t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  fp2_t d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  fp2_t di = fp2_inv(d);
+  return fp6_t{fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ---------------------------------------------------------------------------
+// Fp12
+// ---------------------------------------------------------------------------
+BGV_HD fp12_t fp12_one() { return fp12_t{fp6_one(), fp6_zero()}; }
+
+BGV_HD bool fp12_is_one(const fp12_t& a) {
+  const fp12_t o = fp12_one();
+  bool eq = true;
+  const fp2_t* x = &a.c0.c0;
+  const fp2_t* y = &o.c0.c0;
+  BGV_UNROLL for (int i = 0; i < 6; ++i) eq = eq && fp2_eq(x[i], y[i]);
+  return eq;
+}
+
+BGV_HD fp12_t fp12_conj(const fp12_t& a) { return fp12_t{a.c0, fp6_neg(a.c1)}; }
+
+BGV_HD fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
+  fp6_t t0 = fp6_mul(a.c0, b.c0);
+  fp6_t t1 = fp6_mul(a.c1, b.c1);
+  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
+  return fp12_t{c0, c1};
+}
+
+BGV_HD fp12_t fp12_sqr(const fp12_t& a) {
+  fp6_t t = fp6_mul(a.c0, a.c1);
+  fp6_t s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6_t c0 = fp6_sub(fp6_sub(s, t), fp6_mul_v(t));
+  return fp12_t{c0, fp6_add(t, t)};
+}
+
+// f * (l0 + l1 w^2 + l3 w^3): a line with nonzero tower coefficients
+// c0.c0 = l0, c0.c1 = l1, c1.c1 = l3.
+BGV_HD fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  fp6_t t0 = fp6_mul_01(f.c0, l0, l1);
+  fp6_t t1 = fp6_mul_1(f.c1, l3);
+  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l3)), t0), t1);
+  fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
+  return fp12_t{c0, c1};
+}
+
+BGV_HD fp12_t fp12_inv(const fp12_t& a) {
+  fp6_t n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
+  fp6_t ni = fp6_inv(n);
+  return fp12_t{fp6_mul(a.c0, ni), fp6_neg(fp6_mul(a.c1, ni))};
+}
+
+BGV_HD fp12_t fp12_frob(const fp12_t& a) {
+  const fp2_t g[6] = BGV_FROB1;
+  fp12_t r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), g[1]);
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), g[2]);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), g[3]);
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), g[4]);
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), g[5]);
+  return r;
+}
+
+BGV_HD fp12_t fp12_frob2(const fp12_t& a) {
+  const fp_t g[6] = BGV_FROB2;
+  fp12_t r;
+  r.c0.c0 = a.c0.c0;
+  r.c0.c1 = fp2_mul_fp(a.c0.c1, g[1]);
+  r.c0.c2 = fp2_mul_fp(a.c0.c2, g[2]);
+  r.c1.c0 = fp2_mul_fp(a.c1.c0, g[3]);
+  r.c1.c1 = fp2_mul_fp(a.c1.c1, g[4]);
+  r.c1.c2 = fp2_mul_fp(a.c1.c2, g[5]);
+  return r;
+}
+
+// Granger-Scott squaring, valid in the cyclotomic subgroup (after the easy part).
+BGV_HD void fp4_sqr(fp2_t* c0, fp2_t* c1, const fp2_t& a, const fp2_t& b) {
+  fp2_t t0 = fp2_sqr(a);
+  fp2_t t1 = fp2_sqr(b);
+  *c0 = fp2_add(fp2_mul_xi(t1), t0);
+  *c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+
+BGV_HD fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
+  fp2_t z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
+  fp2_t z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  fp2_t t0, t1, t2, t3;
+  fp4_sqr(&t0, &t1, z0, z1);
+  z0 = fp2_sub(t0, z0);
+  z0 = fp2_add(fp2_dbl(z0), t0);
+  z1 = fp2_add(t1, z1);
+  z1 = fp2_add(fp2_dbl(z1), t1);
+  fp4_sqr(&t0, &t1, z2, z3);
+  fp4_sqr(&t2, &t3, z4, z5);
+  z4 = fp2_sub(t0, z4);
+  z4 = fp2_add(fp2_dbl(z4), t0);
+  z5 = fp2_add(t1, z5);
+  z5 = fp2_add(fp2_dbl(z5), t1);
+  t0 = fp2_mul_xi(t3);
+  z2 = fp2_add(t0, z2);
+  z2 = fp2_add(fp2_dbl(z2), t0);
+  z3 = fp2_sub(t2, z3);
+  z3 = fp2_add(fp2_dbl(z3), t2);
+  return fp12_t{fp6_t{z0, z4, z3}, fp6_t{z2, z1, z5}};
+}

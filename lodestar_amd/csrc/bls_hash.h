@@ -1,0 +1,259 @@
+// hash_to_G2 on CDNA4: RFC 9380 suite BLS12381G2_XMD:SHA-256_SSWU_RO_, one
+// message per lane.  SHA-256 (expand_message_xmd) -> hash_to_field (4 x Fp)
+// -> 2 x simplified SWU on E2' -> 3-isogeny (Jacobian, no inversion) -> add
+// -> clear_cofactor (psi method, RFC 9380 G.4).
+#pragma once
+#include "bls_curve.h"
+
+// ---------------------------------------------------------------------------
+// SHA-256
+// ---------------------------------------------------------------------------
+BGV_HD uint32_t sha_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+BGV_HD void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
+  const uint32_t K[64] = {
+      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+      0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+      0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+      0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+      0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+      0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+      0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+  uint32_t w[16];
+  BGV_UNROLL for (int i = 0; i < 16; ++i) w[i] = blk[i];
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  BGV_UNROLL for (int i = 0; i < 64; ++i) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + K[i] + wi;
+    uint32_t S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+BGV_HD void sha256_init(uint32_t st[8]) {
+  st[0] = 0x6a09e667u;
+  st[1] = 0xbb67ae85u;
+  st[2] = 0x3c6ef372u;
+  st[3] = 0xa54ff53au;
+  st[4] = 0x510e527fu;
+  st[5] = 0x9b05688cu;
+  st[6] = 0x1f83d9abu;
+  st[7] = 0x5be0cd19u;
+}
+
+// Hash a "virtual" message of total_len bytes whose byte at position i is
+// get(i) (lane-uniform length, so every lane runs the same number of blocks).
+template <class G>
+BGV_HD void sha256_virtual(uint32_t out[8], const G& get, uint32_t total_len) {
+  uint32_t st[8];
+  sha256_init(st);
+  const uint32_t padded = ((total_len + 9 + 63) / 64) * 64;
+  const uint64_t bitlen = (uint64_t)total_len * 8;
+  BGV_UNROLL for (uint32_t base = 0; base < padded; base += 64) {
+    uint32_t blk[16];
+    BGV_UNROLL for (int wi = 0; wi < 16; ++wi) {
+      uint32_t word = 0;
+      BGV_UNROLL for (int k = 0; k < 4; ++k) {
+        const uint32_t pos = base + (uint32_t)(wi * 4 + k);
+        uint32_t byte;
+        if (pos < total_len)
+          byte = get(pos);
+        else if (pos == total_len)
+          byte = 0x80;
+        else if (pos >= padded - 8)
+          byte = (uint32_t)(bitlen >> (8 * (padded - 1 - pos))) & 0xff;
+        else
+          byte = 0;
+        word = (word << 8) | byte;
+      }
+      blk[wi] = word;
+    }
+    sha256_compress(st, blk);
+  }
+  BGV_UNROLL for (int i = 0; i < 8; ++i) out[i] = st[i];
+}
+
+BGV_HD uint32_t dst_byte(uint32_t i) {
+  // BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_ || I2OSP(43, 1)
+  const char d[] = BGV_DST_POP;
+  return i < BGV_DST_POP_LEN ? (uint32_t)(uint8_t)d[i] : (uint32_t)BGV_DST_POP_LEN;
+}
+
+struct xmd_b0_getter {
+  const uint8_t* msg;
+  uint32_t len;
+  // Z_pad(64) || msg || I2OSP(256, 2) || 0x00 || DST_prime
+  BGV_HD uint32_t operator()(uint32_t pos) const {
+    if (pos < 64) return 0;
+    pos -= 64;
+    if (pos < len) return msg[pos];
+    pos -= len;
+    if (pos == 0) return 0x01;
+    if (pos == 1) return 0x00;
+    if (pos == 2) return 0x00;
+    return dst_byte(pos - 3);
+  }
+};
+
+struct xmd_bi_getter {
+  const uint32_t* x;  // 8 words (b0 ^ b_{i-1})
+  uint32_t idx;
+  BGV_HD uint32_t operator()(uint32_t pos) const {
+    if (pos < 32) return (x[pos >> 2] >> (24 - 8 * (pos & 3))) & 0xff;
+    if (pos == 32) return idx;
+    return dst_byte(pos - 33);
+  }
+};
+
+// expand_message_xmd(msg, DST_POP, 256) -> 64 big-endian words
+BGV_HD void expand_message_xmd_256(uint32_t ub[64], const uint8_t* msg, uint32_t len) {
+  uint32_t b0[8], bi[8], x[8];
+  xmd_b0_getter g0{msg, len};
+  sha256_virtual(b0, g0, 64 + len + 3 + BGV_DST_POP_LEN + 1);
+  BGV_UNROLL for (int k = 0; k < 8; ++k) x[k] = b0[k];
+  BGV_NO_UNROLL for (uint32_t i = 1; i <= 8; ++i) {
+    xmd_bi_getter gi{x, i};
+    sha256_virtual(bi, gi, 32 + 1 + BGV_DST_POP_LEN + 1);
+    BGV_UNROLL for (int k = 0; k < 8; ++k) {
+      // store b_i: dynamic word index (i-1)*8+k; write via unrolled select to stay in registers
+      x[k] = b0[k] ^ bi[k];
+    }
+    BGV_UNROLL for (int j = 1; j <= 8; ++j) {
+      if (i == (uint32_t)j) {
+        BGV_UNROLL for (int k = 0; k < 8; ++k) ub[(j - 1) * 8 + k] = bi[k];
+      }
+    }
+  }
+}
+
+// 64 big-endian bytes (as 16 words) -> Fp (Montgomery), reduced mod p
+BGV_HD fp_t fp_from_be64_words(const uint32_t* w) {
+  // value = hi * 2^384 + lo, hi = words 0..3 (128 bits), lo = words 4..15 (384 bits)
+  fp_t lo, hi = fp_zero();
+  BGV_UNROLL for (int i = 0; i < NL; ++i) lo.v[i] = w[15 - i];
+  BGV_UNROLL for (int i = 0; i < 4; ++i) hi.v[i] = w[3 - i];
+  const fp_t r2 = {BGV_R2}, r3 = {BGV_R3};
+  return fp_add(fp_mul(lo, r2), fp_mul(hi, r3));
+}
+
+BGV_HD void hash_to_field_fp2(fp2_t* u0, fp2_t* u1, const uint8_t* msg, uint32_t len) {
+  uint32_t ub[64];
+  expand_message_xmd_256(ub, msg, len);
+  u0->c0 = fp_from_be64_words(ub + 0);
+  u0->c1 = fp_from_be64_words(ub + 16);
+  u1->c0 = fp_from_be64_words(ub + 32);
+  u1->c1 = fp_from_be64_words(ub + 48);
+}
+
+// ---------------------------------------------------------------------------
+// Simplified SWU on E2': y^2 = x^3 + A'x + B', A' = 240i, B' = 1012(1+i), Z = -(2+i)
+// ---------------------------------------------------------------------------
+// sqrt(-5) in Fp (Montgomery), used to turn sqrt(-n) into sqrt(N(Z) n), N(Z) = 5.
+BGV_HD fp_t fp_sqrt_minus5() { return fp_t{BGV_SQRT_M5}; }
+
+// If g is a square in Fp2: *y = sqrt(g), returns true.  Otherwise *y = sqrt(Z g).
+// Two Fp exponentiations total (norm root + the Fp2 root).
+BGV_HD bool fp2_sqrt_or_z(fp2_t* y, const fp2_t& g, const fp_t& sqrt_m5) {
+  const fp2_t Z = BGV_SSWU_Z;
+  const fp_t n = fp_add(fp_sqr(g.c0), fp_sqr(g.c1));
+  const fp_t e = fp_pow_p_minus_3_div_4(n);
+  const fp_t ne = fp_mul(n, e);
+  const fp_t s = fp_mul(ne, e);
+  const bool is_sq = fp_eq(s, fp_one()) || fp_is_zero(n);
+  const fp2_t h = fp2_select(is_sq, fp2_mul(Z, g), g);
+  const fp_t gam = fp_select(is_sq, fp_mul(sqrt_m5, fp_neg(ne)), ne);
+  const bool h1z = fp_is_zero(h.c1);
+  fp_t d = fp_select(h1z, fp_half(fp_add(h.c0, gam)), h.c0);
+  fp_t t = fp_pow_p_minus_3_div_4(d);
+  fp_t dt = fp_mul(d, t);
+  fp_t s2 = fp_mul(dt, t);
+  fp_t a1t2 = fp_half(fp_mul(h.c1, t));
+  const bool qr = fp_eq(s2, fp_one());
+  y->c0 = fp_select(qr, a1t2, dt);
+  y->c1 = fp_select(qr, fp_neg(dt), a1t2);
+  return is_sq;
+}
+
+// returns the SWU point on E2' in affine coordinates
+BGV_HD void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
+  const fp2_t A = BGV_SSWU_A, B = BGV_SSWU_B, Z = BGV_SSWU_Z;
+  const fp2_t bza = BGV_SSWU_B_OVER_ZA, mba = BGV_SSWU_MINUS_B_OVER_A;
+  fp2_t u2 = fp2_sqr(u);
+  fp2_t zu2 = fp2_mul(Z, u2);
+  fp2_t den = fp2_add(fp2_sqr(zu2), zu2);
+  const bool den0 = fp2_is_zero(den);
+  fp2_t x1 = fp2_mul(mba, fp2_add(fp2_one(), fp2_inv(den)));
+  x1 = fp2_select(den0, x1, bza);
+  fp2_t gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
+  fp2_t r;
+  const bool sq = fp2_sqrt_or_z(&r, gx1, sqrt_m5);
+  // non-square branch: x2 = Z u^2 x1, y = Z u^3 sqrt(Z gx1)
+  fp2_t x2 = fp2_mul(zu2, x1);
+  fp2_t y2 = fp2_mul(fp2_mul(zu2, u), r);
+  fp2_t x = fp2_select(sq, x2, x1);
+  fp2_t y = fp2_select(sq, y2, r);
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  *xo = x;
+  *yo = y;
+}
+
+// 3-isogeny E2' -> E2 (RFC 9380 E.3), output Jacobian without inversion.
+BGV_HD g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
+  const fp2_t xnum[4] = BGV_ISO_XNUM;
+  const fp2_t xden[2] = BGV_ISO_XDEN;
+  const fp2_t ynum[4] = BGV_ISO_YNUM;
+  const fp2_t yden[3] = BGV_ISO_YDEN;
+  fp2_t x2 = fp2_sqr(x);
+  fp2_t x3 = fp2_mul(x2, x);
+  fp2_t xn = fp2_add(fp2_add(fp2_mul(xnum[3], x3), fp2_mul(xnum[2], x2)), fp2_add(fp2_mul(xnum[1], x), xnum[0]));
+  fp2_t xd = fp2_add(fp2_add(x2, fp2_mul(xden[1], x)), xden[0]);
+  fp2_t yn = fp2_add(fp2_add(fp2_mul(ynum[3], x3), fp2_mul(ynum[2], x2)), fp2_add(fp2_mul(ynum[1], x), ynum[0]));
+  fp2_t yd = fp2_add(fp2_add(x3, fp2_mul(yden[2], x2)), fp2_add(fp2_mul(yden[1], x), yden[0]));
+  g2_jac r;
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(fp2_mul(xn, yd), r.z);
+  r.y = fp2_mul(fp2_mul(fp2_mul(y, yn), xd), fp2_sqr(r.z));
+  return r;
+}
+
+// Full hash_to_G2 of one message: returns Jacobian point in G2.
+BGV_HD g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
+  fp2_t u0, u1;
+  hash_to_field_fp2(&u0, &u1, msg, len);
+  const fp_t sm5 = fp_sqrt_minus5();
+  fp2_t x, y;
+  sswu_g2(&x, &y, u0, sm5);
+  g2_jac q0 = iso_map_g2(x, y);
+  sswu_g2(&x, &y, u1, sm5);
+  g2_jac q1 = iso_map_g2(x, y);
+  return g2_clear_cofactor(jac_add(q0, q1));
+}

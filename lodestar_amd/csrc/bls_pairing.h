@@ -1,0 +1,103 @@
+// Optimal-ate pairing pieces on CDNA4: Miller loop (Jacobian twist point,
+// lines evaluated straight into the sparse Fp12 product) and final
+// exponentiation (easy part + x-chain hard part computing the cube of the
+// pairing, which has the same kernel since gcd(3, r) = 1).
+#pragma once
+#include "bls_curve.h"
+
+// Doubling step: T <- 2T; returns the tangent line at T evaluated at P,
+// scaled by Fp2/Fp4 factors that the final exponentiation kills:
+//   l0 = 3X^3 - 2Y^2,  l1 = -3X^2 Z^2 xP,  l3 = Z3 Z^2 yP
+BGV_HD void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const fp_t& xp_neg, const fp_t& yp) {
+  fp2_t A = fp2_sqr(t.x);
+  fp2_t B = fp2_sqr(t.y);
+  fp2_t C = fp2_sqr(B);
+  fp2_t ZZ = fp2_sqr(t.z);
+  fp2_t D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.x, B)), A), C));
+  fp2_t E = fp2_add(fp2_dbl(A), A);
+  fp2_t F = fp2_sqr(E);
+  *l0 = fp2_sub(fp2_mul(E, t.x), fp2_dbl(B));
+  *l1 = fp2_mul_fp(fp2_mul(E, ZZ), xp_neg);
+  fp2_t X3 = fp2_sub(F, fp2_dbl(D));
+  fp2_t Y3 = fp2_sub(fp2_mul(E, fp2_sub(D, X3)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
+  fp2_t Z3 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.y, t.z)), B), ZZ);
+  *l3 = fp2_mul_fp(fp2_mul(Z3, ZZ), yp);
+  t.x = X3;
+  t.y = Y3;
+  t.z = Z3;
+}
+
+// Addition step: T <- T + Q (Q affine); returns the chord line at P:
+//   l0 = r xQ - yQ Z3,  l1 = -r xP,  l3 = Z3 yP   (r = 2(S2 - Y))
+BGV_HD void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const g2_aff& q, const fp_t& xp_neg,
+                       const fp_t& yp) {
+  fp2_t ZZ = fp2_sqr(t.z);
+  fp2_t U2 = fp2_mul(q.x, ZZ);
+  fp2_t S2 = fp2_mul(q.y, fp2_mul(t.z, ZZ));
+  fp2_t H = fp2_sub(U2, t.x);
+  fp2_t HH = fp2_sqr(H);
+  fp2_t I = fp2_dbl(fp2_dbl(HH));
+  fp2_t J = fp2_mul(H, I);
+  fp2_t r = fp2_dbl(fp2_sub(S2, t.y));
+  fp2_t V = fp2_mul(t.x, I);
+  fp2_t X3 = fp2_sub(fp2_sub(fp2_sqr(r), J), fp2_dbl(V));
+  fp2_t Y3 = fp2_sub(fp2_mul(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul(t.y, J)));
+  fp2_t Z3 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.z, H)), ZZ), HH);
+  *l0 = fp2_sub(fp2_mul(r, q.x), fp2_mul(q.y, Z3));
+  *l1 = fp2_mul_fp(r, xp_neg);
+  *l3 = fp2_mul_fp(Z3, yp);
+  t.x = X3;
+  t.y = Y3;
+  t.z = Z3;
+}
+
+// f_{|x|,Q}(P), conjugated for x < 0.  P = (xP, yP) in G1, Q in G2, both affine
+// and not infinity.  Loop over the bits of |x| = 0xd201000000010000 below the top.
+BGV_HD fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
+  const fp_t xp_neg = fp_neg(p.x);
+  const fp_t yp = p.y;
+  g2_jac t = jac_from_aff(q);
+  fp12_t f = fp12_one();
+  fp2_t l0, l1, l3;
+  const uint64_t X = BGV_X_ABS;
+  // first doubling: f = 1, so f^2 * line = line
+  miller_dbl(t, &l0, &l1, &l3, xp_neg, yp);
+  f = fp12_mul_line(f, l0, l1, l3);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if ((X >> (i + 1)) & 1) {
+      miller_add(t, &l0, &l1, &l3, q, xp_neg, yp);
+      f = fp12_mul_line(f, l0, l1, l3);
+    }
+    f = fp12_sqr(f);
+    miller_dbl(t, &l0, &l1, &l3, xp_neg, yp);
+    f = fp12_mul_line(f, l0, l1, l3);
+  }
+  // bit 0 of |x| is 0: no trailing addition
+  return fp12_conj(f);
+}
+
+// a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
+BGV_HD fp12_t cyclotomic_pow_x(const fp12_t& a) {
+  const uint64_t X = BGV_X_ABS;
+  fp12_t r = a;
+  BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {
+    r = fp12_cyclotomic_sqr(r);
+    if ((X >> i) & 1) r = fp12_mul(r, a);
+  }
+  return fp12_conj(r);
+}
+
+// f^(3 (p^12 - 1) / r) using 3 (p^4 - p^2 + 1)/r = (x-1)^2 (x+p) (x^2+p^2-1) + 3
+BGV_HD fp12_t final_exp(const fp12_t& f) {
+  // easy part: f^((p^6 - 1)(p^2 + 1))
+  fp12_t t = fp12_mul(fp12_conj(f), fp12_inv(f));
+  t = fp12_mul(fp12_frob2(t), t);
+  // hard part
+  fp12_t a = fp12_mul(cyclotomic_pow_x(t), fp12_conj(t));  // t^(x-1)
+  a = fp12_mul(cyclotomic_pow_x(a), fp12_conj(a));         // t^((x-1)^2)
+  a = fp12_mul(cyclotomic_pow_x(a), fp12_frob(a));         // ^(x+p)
+  fp12_t b = cyclotomic_pow_x(cyclotomic_pow_x(a));        // a^(x^2)
+  b = fp12_mul(fp12_mul(b, fp12_frob2(a)), fp12_conj(a));  // a^(x^2 + p^2 - 1)
+  fp12_t t3 = fp12_mul(fp12_cyclotomic_sqr(t), t);         // t^3
+  return fp12_mul(b, t3);
+}

@@ -1,0 +1,158 @@
+// TEST-ONLY host build of the device arithmetic (lodestar_amd/csrc/bls_*.h).
+//
+// The kernels' per-lane math is plain C++ in __host__ __device__ headers, so
+// the exact same formulas are compiled here with g++ and exercised from
+// pytest against oracle/bls12381.py on a machine without a GPU.  Nothing in
+// the product links this library; the product path is the HIP build only.
+#include <string.h>
+
+#include "../../lodestar_amd/csrc/bls_hash.h"
+#include "../../lodestar_amd/csrc/bls_pairing.h"
+
+static fp_t in_fp(const uint8_t* be) { return fp_to_mont(fp_from_be48(be)); }
+static void out_fp(uint8_t* be, const fp_t& a) { fp_to_be48(be, fp_from_mont(a)); }
+static fp2_t in_fp2(const uint8_t* be) { return fp2_t{in_fp(be), in_fp(be + 48)}; }  // (c0, c1)
+static void out_fp2(uint8_t* be, const fp2_t& a) {
+  out_fp(be, a.c0);
+  out_fp(be + 48, a.c1);
+}
+static void out_fp12(uint8_t* be, const fp12_t& f) {
+  const fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; ++i) out_fp2(be + 96 * i, *c[i]);
+}
+static fp12_t in_fp12(const uint8_t* be) {
+  fp12_t f;
+  fp2_t* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  for (int i = 0; i < 6; ++i) *c[i] = in_fp2(be + 96 * i);
+  return f;
+}
+// G2 affine as x.c0 | x.c1 | y.c0 | y.c1 (48 B each, raw BE) -- test layout
+static g2_aff in_g2(const uint8_t* be) { return g2_aff{in_fp2(be), in_fp2(be + 96)}; }
+static void out_g2(uint8_t* be, const g2_aff& a) {
+  out_fp2(be, a.x);
+  out_fp2(be + 96, a.y);
+}
+static g1_aff in_g1(const uint8_t* be) { return g1_aff{in_fp(be), in_fp(be + 48)}; }
+static void out_g1(uint8_t* be, const g1_aff& a) {
+  out_fp(be, a.x);
+  out_fp(be + 48, a.y);
+}
+
+extern "C" {
+
+void hs_fp_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_mul(in_fp(a), in_fp(b))); }
+void hs_fp_add(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_add(in_fp(a), in_fp(b))); }
+void hs_fp_sub(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_sub(in_fp(a), in_fp(b))); }
+void hs_fp_neg(uint8_t* r, const uint8_t* a) { out_fp(r, fp_neg(in_fp(a))); }
+void hs_fp_inv(uint8_t* r, const uint8_t* a) { out_fp(r, fp_inv(in_fp(a))); }
+void hs_fp_half(uint8_t* r, const uint8_t* a) { out_fp(r, fp_half(in_fp(a))); }
+int hs_fp_sqrt(uint8_t* r, const uint8_t* a) {
+  fp_t s;
+  int ok = fp_sqrt(&s, in_fp(a));
+  out_fp(r, s);
+  return ok;
+}
+void hs_fp2_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp2(r, fp2_mul(in_fp2(a), in_fp2(b))); }
+void hs_fp2_sqr(uint8_t* r, const uint8_t* a) { out_fp2(r, fp2_sqr(in_fp2(a))); }
+void hs_fp2_inv(uint8_t* r, const uint8_t* a) { out_fp2(r, fp2_inv(in_fp2(a))); }
+int hs_fp2_sqrt(uint8_t* r, const uint8_t* a) {
+  fp2_t s;
+  int ok = fp2_sqrt(&s, in_fp2(a));
+  out_fp2(r, s);
+  return ok;
+}
+int hs_fp2_sgn0(const uint8_t* a) { return (int)fp2_sgn0(in_fp2(a)); }
+void hs_fp12_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp12(r, fp12_mul(in_fp12(a), in_fp12(b))); }
+void hs_fp12_sqr(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_sqr(in_fp12(a))); }
+void hs_fp12_inv(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_inv(in_fp12(a))); }
+void hs_fp12_frob(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_frob(in_fp12(a))); }
+void hs_fp12_frob2(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_frob2(in_fp12(a))); }
+void hs_fp12_cyc_sqr(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_cyclotomic_sqr(in_fp12(a))); }
+void hs_fp12_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
+  out_fp12(r, fp12_mul_line(in_fp12(f), in_fp2(l0), in_fp2(l1), in_fp2(l3)));
+}
+
+// G2 compressed (96 B) -> test-layout affine (192 B); returns BGV code, 100 = infinity
+int hs_g2_decompress(uint8_t* out, const uint8_t* in) {
+  g2_aff a;
+  bool inf;
+  int rc = g2_decompress(&a, &inf, in);
+  if (rc) return rc;
+  if (inf) return 100;
+  out_g2(out, a);
+  return 0;
+}
+void hs_g2_compress(uint8_t* out96, const uint8_t* aff) { g2_compress(out96, in_g2(aff), false); }
+int hs_g2_in_subgroup(const uint8_t* aff) { return g2_in_subgroup(jac_from_aff(in_g2(aff))); }
+int hs_g2_on_curve(const uint8_t* aff) { return g2_aff_on_curve(in_g2(aff)); }
+
+static int g2_out(uint8_t* out, const g2_jac& j) {
+  g2_aff a;
+  if (!jac_to_aff(&a, j)) return 0;
+  out_g2(out, a);
+  return 1;
+}
+static int g1_out(uint8_t* out, const g1_jac& j) {
+  g1_aff a;
+  if (!jac_to_aff(&a, j)) return 0;
+  out_g1(out, a);
+  return 1;
+}
+
+int hs_g2_mul_u64(uint8_t* out, const uint8_t* aff, uint64_t k) {
+  return g2_out(out, jac_mul_u64(jac_from_aff(in_g2(aff)), k));
+}
+int hs_g2_add(uint8_t* out, const uint8_t* a, const uint8_t* b) {
+  return g2_out(out, jac_add(jac_from_aff(in_g2(a)), jac_from_aff(in_g2(b))));
+}
+int hs_g2_dbl(uint8_t* out, const uint8_t* a) { return g2_out(out, jac_dbl(jac_from_aff(in_g2(a)))); }
+int hs_g2_psi(uint8_t* out, const uint8_t* a) { return g2_out(out, g2_psi(jac_from_aff(in_g2(a)))); }
+int hs_g2_clear_cofactor(uint8_t* out, const uint8_t* a) {
+  return g2_out(out, g2_clear_cofactor(jac_from_aff(in_g2(a))));
+}
+int hs_g1_mul_u64(uint8_t* out, const uint8_t* aff, uint64_t k) {
+  return g1_out(out, jac_mul_u64(jac_from_aff(in_g1(aff)), k));
+}
+int hs_g1_add(uint8_t* out, const uint8_t* a, const uint8_t* b) {
+  return g1_out(out, jac_add(jac_from_aff(in_g1(a)), jac_from_aff(in_g1(b))));
+}
+
+void hs_hash_to_field(uint8_t* out4x48, const uint8_t* msg, uint32_t len) {
+  fp2_t u0, u1;
+  hash_to_field_fp2(&u0, &u1, msg, len);
+  out_fp2(out4x48, u0);
+  out_fp2(out4x48 + 96, u1);
+}
+void hs_sswu(uint8_t* out, const uint8_t* u) {
+  fp2_t x, y;
+  sswu_g2(&x, &y, in_fp2(u), fp_sqrt_minus5());
+  out_g2(out, g2_aff{x, y});
+}
+int hs_iso_map(uint8_t* out, const uint8_t* aff) {
+  g2_aff a = in_g2(aff);
+  return g2_out(out, iso_map_g2(a.x, a.y));
+}
+int hs_hash_to_g2(uint8_t* out_aff, uint8_t* out_comp96, const uint8_t* msg, uint32_t len) {
+  g2_aff a;
+  g2_jac h = hash_to_g2(msg, len);
+  if (!jac_to_aff(&a, h)) return 0;
+  out_g2(out_aff, a);
+  g2_compress(out_comp96, a, false);
+  return 1;
+}
+
+// P (test layout g1) , Q (test layout g2) -> Miller loop value and pairing^3
+void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12(out, miller_loop(in_g1(p), in_g2(q))); }
+void hs_final_exp(uint8_t* out, const uint8_t* f) { out_fp12(out, final_exp(in_fp12(f))); }
+
+int hs_g1_decompress(uint8_t* out, const uint8_t* in48) {
+  g1_aff a;
+  bool inf;
+  int rc = g1_decompress(&a, &inf, in48);
+  if (rc) return rc;
+  if (inf) return 100;
+  out_g1(out, a);
+  return 0;
+}
+void hs_g1_serialize(uint8_t* out96, const uint8_t* aff) { g1_serialize(out96, in_g1(aff), false); }
+}

@@ -1,0 +1,252 @@
+"""CPU unit tests of the kernel math (lodestar_amd/csrc/bls_*.h compiled for the
+host as tests/native/libhostsim.so) against the oracle, oracle/bls12381.py.
+
+Every device formula — Montgomery CIOS, Fp2 sqrt, line functions, Miller
+loop, final exponentiation, SSWU/iso/cofactor, ZCash decoding — is checked
+here bit-for-bit before it ever runs on an MI355X.
+"""
+import random
+
+import pytest
+
+from oracle import bls12381 as o
+from tests import hostsim as hs
+
+rnd = random.Random(0xB15)
+P = o.P
+
+
+def rfp():
+    return rnd.randrange(P)
+
+
+def rfp2():
+    return (rfp(), rfp())
+
+
+@pytest.fixture(scope="module")
+def L():
+    return hs.lib()
+
+
+def test_fp_ops(L):
+    for _ in range(50):
+        a, b = rfp(), rfp()
+        r = hs.buf(48)
+        L.hs_fp_mul(r, hs.fp_b(a), hs.fp_b(b))
+        assert hs.b_fp(r.raw) == a * b % P
+        L.hs_fp_add(r, hs.fp_b(a), hs.fp_b(b))
+        assert hs.b_fp(r.raw) == (a + b) % P
+        L.hs_fp_sub(r, hs.fp_b(a), hs.fp_b(b))
+        assert hs.b_fp(r.raw) == (a - b) % P
+        L.hs_fp_neg(r, hs.fp_b(a))
+        assert hs.b_fp(r.raw) == (-a) % P
+        L.hs_fp_half(r, hs.fp_b(a))
+        assert hs.b_fp(r.raw) * 2 % P == a
+    for a in (0, 1, P - 1, 2**380, P // 2):
+        r = hs.buf(48)
+        L.hs_fp_mul(r, hs.fp_b(a), hs.fp_b(P - 1))
+        assert hs.b_fp(r.raw) == a * (P - 1) % P
+        L.hs_fp_neg(r, hs.fp_b(a))
+        assert hs.b_fp(r.raw) == (-a) % P
+    a = rfp()
+    r = hs.buf(48)
+    L.hs_fp_inv(r, hs.fp_b(a))
+    assert hs.b_fp(r.raw) * a % P == 1
+
+
+def test_fp_sqrt(L):
+    for _ in range(8):
+        a = rfp()
+        r = hs.buf(48)
+        ok = L.hs_fp_sqrt(r, hs.fp_b(a))
+        assert bool(ok) == o.fp_is_square(a)
+        if ok:
+            assert hs.b_fp(r.raw) ** 2 % P == a
+
+
+def test_fp2_ops(L):
+    for _ in range(20):
+        a, b = rfp2(), rfp2()
+        r = hs.buf(96)
+        L.hs_fp2_mul(r, hs.fp2_b(a), hs.fp2_b(b))
+        assert hs.b_fp2(r.raw) == o.f2_mul(a, b)
+        L.hs_fp2_sqr(r, hs.fp2_b(a))
+        assert hs.b_fp2(r.raw) == o.f2_sqr(a)
+    a = rfp2()
+    r = hs.buf(96)
+    L.hs_fp2_inv(r, hs.fp2_b(a))
+    assert o.f2_mul(hs.b_fp2(r.raw), a) == (1, 0)
+
+
+def test_fp2_sqrt(L):
+    cases = [rfp2() for _ in range(8)] + [(rfp(), 0), (0, rfp()), (0, 0), (4, 0), (P - 4, 0)]
+    cases += [o.f2_sqr(rfp2()) for _ in range(4)]
+    for a in cases:
+        r = hs.buf(96)
+        ok = L.hs_fp2_sqrt(r, hs.fp2_b(a))
+        assert bool(ok) == o.f2_is_square(a), a
+        if ok:
+            assert o.f2_sqr(hs.b_fp2(r.raw)) == (a[0] % P, a[1] % P)
+
+
+def rand_f12():
+    return tuple(rfp2() for _ in range(6))
+
+
+def f12_tower_bytes(f):
+    return hs.fp12_b_tower(o.f12_to_tower_list(f))
+
+
+def test_fp12_ops(L):
+    a, b = rand_f12(), rand_f12()
+    r = hs.buf(576)
+    L.hs_fp12_mul(r, f12_tower_bytes(a), f12_tower_bytes(b))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_mul(a, b))
+    L.hs_fp12_sqr(r, f12_tower_bytes(a))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_sqr(a))
+    L.hs_fp12_frob(r, f12_tower_bytes(a))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_frob(a))
+    L.hs_fp12_frob2(r, f12_tower_bytes(a))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_frob(o.f12_frob(a)))
+    L.hs_fp12_inv(r, f12_tower_bytes(a))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_inv_fast(a))
+    # sparse line product: l0 at w^0, l1 at w^2, l3 at w^3
+    l0, l1, l3 = rfp2(), rfp2(), rfp2()
+    line = (l0, o.F2_ZERO, l1, l3, o.F2_ZERO, o.F2_ZERO)
+    L.hs_fp12_mul_line(r, f12_tower_bytes(a), hs.fp2_b(l0), hs.fp2_b(l1), hs.fp2_b(l3))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_mul(a, line))
+
+
+def test_cyclotomic_sqr(L):
+    a = rand_f12()
+    # project into the cyclotomic subgroup with the easy part
+    t = o.f12_mul(o.f12_conj(a), o.f12_inv_fast(a))
+    t = o.f12_mul(o.f12_frob(o.f12_frob(t)), t)
+    r = hs.buf(576)
+    L.hs_fp12_cyc_sqr(r, f12_tower_bytes(t))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_sqr(t))
+
+
+def g2_rand_in_group():
+    return o.g2_mul(o.G2, rnd.randrange(1, o.R))
+
+
+def test_g2_arith(L):
+    q1, q2 = g2_rand_in_group(), g2_rand_in_group()
+    r = hs.buf(192)
+    assert L.hs_g2_add(r, hs.g2_b(q1), hs.g2_b(q2))
+    assert hs.b_g2(r.raw) == o.g2_add(q1, q2)
+    assert L.hs_g2_add(r, hs.g2_b(q1), hs.g2_b(q1))  # equal inputs -> doubling
+    assert hs.b_g2(r.raw) == o.g2_add(q1, q1)
+    assert not L.hs_g2_add(r, hs.g2_b(q1), hs.g2_b(o.g2_neg(q1)))  # -> infinity
+    assert L.hs_g2_dbl(r, hs.g2_b(q1))
+    assert hs.b_g2(r.raw) == o.g2_add(q1, q1)
+    for k in (1, 2, 3, 5, 0xFFFFFFFFFFFFFFFF, rnd.getrandbits(64)):
+        assert L.hs_g2_mul_u64(r, hs.g2_b(q1), hs.ctypes.c_uint64(k))
+        assert hs.b_g2(r.raw) == o.g2_mul(q1, k)
+    assert L.hs_g2_psi(r, hs.g2_b(q1))
+    assert hs.b_g2(r.raw) == o.g2_psi(q1)
+
+
+def test_g2_subgroup_and_cofactor(L):
+    q = g2_rand_in_group()
+    assert L.hs_g2_in_subgroup(hs.g2_b(q)) == 1
+    nq = o.map_to_curve_g2(rfp2())  # on E2, (almost surely) not in G2
+    assert o.g2_on_curve(nq)
+    assert L.hs_g2_on_curve(hs.g2_b(nq)) == 1
+    assert L.hs_g2_in_subgroup(hs.g2_b(nq)) == 0
+    r = hs.buf(192)
+    assert L.hs_g2_clear_cofactor(r, hs.g2_b(nq))
+    cc = hs.b_g2(r.raw)
+    assert cc == o.clear_cofactor_g2(nq)
+    assert L.hs_g2_in_subgroup(hs.g2_b(cc)) == 1
+
+
+def test_g1_arith(L):
+    p1 = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    p2 = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    r = hs.buf(96)
+    assert L.hs_g1_add(r, hs.g1_b(p1), hs.g1_b(p2))
+    assert hs.b_g1(r.raw) == o.g1_add(p1, p2)
+    k = rnd.getrandbits(64)
+    assert L.hs_g1_mul_u64(r, hs.g1_b(p1), hs.ctypes.c_uint64(k))
+    assert hs.b_g1(r.raw) == o.g1_mul(p1, k)
+
+
+def test_hash_to_g2_pieces(L):
+    msg = bytes(range(32))
+    r = hs.buf(192)
+    L.hs_hash_to_field(r, msg, 32)
+    u0, u1 = o.hash_to_field_fp2(msg, o.DST_POP)
+    assert hs.b_g2(r.raw) == (u0, u1)
+    for u in (u0, u1, rfp2(), rfp2(), rfp2()):
+        L.hs_sswu(r, hs.fp2_b(u))
+        assert hs.b_g2(r.raw) == o.sswu_g2(u)
+    pt = o.sswu_g2(u0)
+    assert L.hs_iso_map(r, hs.g2_b(pt))
+    assert hs.b_g2(r.raw) == o.iso_map_g2(pt)
+
+
+@pytest.mark.parametrize("msg", [b"", b"abc", bytes(32), bytes([7]) * 32, bytes(range(100))])
+def test_hash_to_g2(L, msg):
+    aff, comp = hs.buf(192), hs.buf(96)
+    assert L.hs_hash_to_g2(aff, comp, msg, len(msg))
+    h = o.hash_to_g2(msg)
+    assert hs.b_g2(aff.raw) == h
+    assert comp.raw == o.g2_compress(h)
+
+
+def test_g2_decompress(L):
+    q = g2_rand_in_group()
+    comp = o.g2_compress(q)
+    r = hs.buf(192)
+    assert L.hs_g2_decompress(r, comp) == 0
+    assert hs.b_g2(r.raw) == q
+    c = hs.buf(96)
+    L.hs_g2_compress(c, hs.g2_b(q))
+    assert c.raw == comp
+    # infinity
+    assert L.hs_g2_decompress(r, bytes([0xC0]) + bytes(95)) == 100
+    # bad flags / non-canonical / off-curve
+    assert L.hs_g2_decompress(r, bytes([0x00]) + comp[1:]) == o.BLST_BAD_ENCODING
+    assert L.hs_g2_decompress(r, bytes([0xC0]) + bytes(94) + b"\x01") == o.BLST_BAD_ENCODING
+    big = bytearray(comp)
+    big[0] = 0x80 | 0x1F
+    big[1:48] = b"\xff" * 47
+    assert L.hs_g2_decompress(r, bytes(big)) == o.BLST_BAD_ENCODING
+    # find an x that is not on the curve
+    for k in range(1, 50):
+        cand = bytearray(comp)
+        cand[95] ^= k
+        try:
+            o.g2_decompress(bytes(cand))
+        except o.BlstError as e:
+            assert L.hs_g2_decompress(r, bytes(cand)) == e.code
+            break
+
+
+def test_g1_decompress(L, golden_dir):
+    import json
+    import os
+    pks = json.load(open(os.path.join(golden_dir, "interop-pubkeys.json")))
+    r = hs.buf(96)
+    for h in pks[:5]:
+        b = bytes.fromhex(h[2:])
+        assert L.hs_g1_decompress(r, b) == 0
+        pt = hs.b_g1(r.raw)
+        assert pt == o.g1_decompress(b)
+        s = hs.buf(96)
+        L.hs_g1_serialize(s, hs.g1_b(pt))
+        assert s.raw == o.g1_serialize(pt)
+
+
+def test_pairing(L):
+    p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    q = g2_rand_in_group()
+    ml = hs.buf(576)
+    L.hs_miller_loop(ml, hs.g1_b(p), hs.g2_b(q))
+    fe = hs.buf(576)
+    L.hs_final_exp(fe, ml.raw)
+    want = o.f12_pow(o.pairing(p, q), 3)  # device final exp computes e(P,Q)^3
+    assert hs.b_fp12_tower(fe.raw) == o.f12_to_tower_list(want)
