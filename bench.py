@@ -1,0 +1,224 @@
+"""Benchmark: verified signature sets/sec at 8192-set batches (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip8192|agg1024|block|...]
+
+A step = one pass of the hot path over one synthetic batch: bgv_verify of 8192
+signature sets (config 4: gossip shape, 8192 batchable one-set jobs, 1 %
+corrupted so the batch-fail -> per-job retry path runs), inputs already resident
+(pubkey cache on the device, set records in host memory as the C-ABI takes them).
+For N > 1 (torchrun) every rank verifies its own 8192-set batches on its own GPU
+(sets shard with no data-path exchange: scaling "weak"); the slowest rank's time
+is the job time.  Verdicts of every step are checked against the expected codes
+(known by construction, the corruption classes pinned by tests/test_gpu_parity.py).
+
+The JSON line carries:
+  roofline     integer-VALU roofline of the dominant kernel: algorithmic u32 MACs
+               (Fp-mul-eq counted in profiles/opcounts.json x 288) / its HIP-event time,
+               against the gfx950 peak v_mad_u64_u32 rate (16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz)
+  cpu_baseline the CPU oracle (oracle/bls12381.py, pure Python, 1 core) on a bounded sample
+"""
+import argparse
+import hashlib
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+PEAK_MAC_PER_S = 1024 * 16 * 2.4e9  # v_mad_u64_u32: half rate on SIMD-32 (tools/ubench_valu.hip)
+MACS_PER_FP_MUL = 288
+
+
+def interop_sk(i: int) -> bytes:
+    """state-transition/src/util/interop.ts:19-22"""
+    d = hashlib.sha256(i.to_bytes(32, "little")).digest()
+    return (int.from_bytes(d, "little") % R_ORDER).to_bytes(32, "big")
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+class Barrier:
+    def __init__(self, world):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", init_method="env://")
+            self.dist = dist
+
+    def __call__(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cuda_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0x8192):
+    """config 4: nsets single sets over distinct validators, distinct signing roots,
+    1 % corrupted at random.Random(0x8192).sample positions, three classes."""
+    key_of = [(rank * nsets + i * 7919) % nkeys for i in range(nsets)]
+    msgs = [hashlib.sha256(b"lodestar-bench" + rank.to_bytes(4, "little") + i.to_bytes(4, "little")).digest()
+            for i in range(nsets)]
+    sigs_raw = ctx.sign(b"".join(interop_sk(k) for k in key_of), b"".join(msgs))
+    sigs = [sigs_raw[96 * i:96 * i + 96] for i in range(nsets)]
+    expect = [1] * nsets
+    bad = random.Random(seed).sample(range(nsets), int(round(nsets * corrupt_frac)))
+    for j, i in enumerate(bad):
+        if j % 3 == 0:
+            msgs[i] = hashlib.sha256(b"wrong" + msgs[i]).digest()
+            expect[i] = 0
+        elif j % 3 == 1:
+            key_of[i] = (key_of[i] + 1) % nkeys
+            expect[i] = 0
+        else:
+            sigs[i] = bytes([sigs[i][0] & 0x7F]) + sigs[i][1:]
+            expect[i] = -1
+    jobs = [([native.SetSpec(msgs[i], sigs[i], pk_indices=[key_of[i]])], True) for i in range(nsets)]
+    return jobs, expect
+
+
+def cpu_baseline_oracle(n=4):
+    """Pure-Python oracle batch verify of n single sets (1 core), bounded sample."""
+    from oracle import bls12381 as o
+    sks = [o.interop_secret_key(i) for i in range(n)]
+    msgs = [hashlib.sha256(b"cpu-%d" % i).digest() for i in range(n)]
+    sets = [(o.sk_to_pk(sks[i]), msgs[i], o.g2_compress(o.sign(sks[i], msgs[i]))) for i in range(n)]
+    t0 = time.perf_counter()
+    ok = o.verify_signature_sets_maybe_batch(sets)
+    dt = time.perf_counter() - t0
+    assert ok
+    return {"value": n / dt, "unit": "sets/s", "cores": 1, "kind": "port",
+            "sample": "oracle/bls12381.py verifyMultipleSignatures of %d single sets (pure Python big ints), "
+                      "%.1f s" % (n, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nsets", type=int, default=8192)
+    ap.add_argument("--nkeys", type=int, default=131072)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    rank, world, local = dist_env()
+    barrier = Barrier(world)
+
+    from lodestar_amd import native
+    ctx = native.Context([local])
+    # device-resident pubkey cache of nkeys interop validators
+    t0 = time.perf_counter()
+    ctx.keygen(b"".join(interop_sk(i) for i in range(args.nkeys)), cache_first=0, want_pubkeys=False)
+    jobs, expect = make_gossip_batch(ctx, native, rank, args.nsets, args.nkeys)
+    setup_s = time.perf_counter() - t0
+    packed = native.PackedCall(jobs)
+
+    def step():
+        out = (native.ctypes.c_int32 * len(jobs))()
+        st = native.BgvStats()
+        rc = ctx.lib.bgv_verify(ctx.handle, packed.jobs, len(jobs), packed.sets, packed.nsets, native.MODE_WORKER,
+                                out, native.ctypes.byref(st))
+        if rc != 0:
+            raise native.DeviceError(native.strerror(rc))
+        return list(out), st
+
+    for _ in range(args.warmup):
+        got, _ = step()
+        assert got == expect, "verdict mismatch in warmup"
+    ctx.profile(1)
+    barrier()
+    cuda_sync()
+    lat = []
+    t_start = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        got, st = step()
+        lat.append(time.perf_counter() - ts)
+        stats.append(st)
+        if got != expect:
+            raise SystemExit("verdict mismatch")
+    cuda_sync()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    elapsed = barrier.max(elapsed)
+    kms, launches = ctx.profile(0)
+
+    if rank == 0:
+        total_sets = args.nsets * args.steps * world
+        opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["fp_mul_eq"]
+        per_set = {"k_sig": opc["k_sig"], "k_hash": opc["k_hash"], "k_pk": opc["k_pk[n_pk=1]"],
+                   "k_miller": opc["k_miller"]}
+        avg = {k: v / max(1, launches) for k, v in kms.items()}
+        dom = max(per_set, key=lambda k: avg.get(k, 0))
+        # sets launched per verify call (first pass + retries), averaged
+        slots = statistics.mean(s.sets_verified for s in stats)
+        achieved = per_set[dom] * MACS_PER_FP_MUL * slots / (avg[dom] * 1e-3)
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tf):
+            traffic = json.load(open(tf)).get(dom)
+        line = {
+            "metric": "verified signature sets/sec (node) at 8192-set batches",
+            "value": total_sets / elapsed,
+            "unit": "sets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "p50_batch_latency_ms": 1e3 * statistics.median(lat),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (28-bit-limb Montgomery Fp, v_mad_u64_u32)",
+            "data": "synthetic: interop validator keys (%d in the device cache), distinct 32-B signing roots, "
+                    "device-signed; 1%% corrupted (wrong msg / wrong key / bad encoding)" % args.nkeys,
+            "config": {"workload": "config4: 8192-set gossip batch (8192 batchable one-set jobs, BGV_MODE_WORKER, "
+                                   "batch-fail -> per-job retry)", "sets_per_batch": args.nsets,
+                       "parallelism": "dp%d (independent batches per GPU)" % world},
+            "kernel_ms_per_launch": avg,
+            "retries_per_step": statistics.mean(s.batch_retries for s in stats),
+            "device_groups_per_step": statistics.mean(s.device_groups for s in stats),
+            "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
+                         "unit": "TMAC/s (u32 mad)", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
+                         "work_per_set": "%d Fp-mul-eq x %d MAC" % (per_set[dom], MACS_PER_FP_MUL)},
+            "setup_s": setup_s,
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_oracle()
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    barrier.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+/*
+ * blsgpu.h — C-ABI of the MI355X batch BLS12-381 signature-set verifier
+ * (libblsgpu.so).  Drop-in engine behind Lodestar's IBlsVerifier:
+ *
+ *   packages/beacon-node/src/chain/bls/interface.ts:20-46
+ *     verifySignatureSets(sets: ISignatureSet[], opts?: VerifySignatureOpts): Promise<boolean>
+ *     close(): Promise<void>
+ *
+ * Each entry point below names the reference function it replaces.  The
+ * reference holds no native code of its own: the arithmetic lives in the
+ * un-vendored dependency @chainsafe/bls@7.1.1 -> @chainsafe/blst@0.2.4 ->
+ * supranational blst (yarn.lock:458-473), which this library re-implements as
+ * HIP kernels for gfx950.
+ *
+ * Conventions: plain C, no exceptions cross the boundary, every function
+ * returns an int status (BGV_OK = 0, negative = call failed, see bgv_strerror).
+ * Verdict codes per job are 1 (valid), 0 (invalid) or -code where code is one
+ * of the BLST-numbered errors below.  One context per process; calls on one
+ * context are serialised internally.
+ */
+#ifndef BLSGPU_H
+#define BLSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes.  1..8 follow blst's BLST_ERROR enum (the message of the
+ * rejected Promise contains the name, e.g. "BLST_INVALID_SIZE",
+ * beacon-node/test/e2e/chain/bls/multithread.test.ts:86-103). */
+enum {
+  BGV_OK = 0,
+  BGV_BLST_BAD_ENCODING = 1,
+  BGV_BLST_POINT_NOT_ON_CURVE = 2,
+  BGV_BLST_POINT_NOT_IN_GROUP = 3,
+  BGV_BLST_AGGR_TYPE_MISMATCH = 4,
+  BGV_BLST_VERIFY_FAIL = 5,
+  BGV_BLST_PK_IS_INFINITY = 6,
+  BGV_BLST_BAD_SCALAR = 7,
+  BGV_BLST_INVALID_SIZE = 8,
+  BGV_E_EMPTY_AGGREGATE = 20, /* PublicKey.aggregate([]) — "EMPTY_AGGREGATE_ARRAY" (chain/bls/utils.ts:11) */
+  BGV_E_EMPTY_SET = 21,       /* "Empty signature set" (chain/bls/maybeBatch.ts:29-31) */
+  BGV_E_BAD_INDEX = 22,       /* validator index not in the device pubkey cache */
+  BGV_E_ARG = 23,             /* malformed call */
+  BGV_E_DEVICE = 30,          /* HIP error: never reported as a verdict */
+  BGV_E_NOMEM = 31,
+  BGV_E_CLOSED = 32           /* QueueError QUEUE_ABORTED after close() (multithread/index.ts:176-186,239-241) */
+};
+
+/* Verification modes of bgv_verify. */
+enum {
+  /* BlsMultiThreadWorkerPool worker semantics (multithread/worker.ts:32-108):
+   * batchable jobs are verified together, and when a device group that mixes
+   * jobs fails, every job in it is re-verified alone; non-batchable jobs are
+   * verified alone (no retry). */
+  BGV_MODE_WORKER = 0,
+  /* every job verified alone (verifySignatureSetsMaybeBatch per job,
+   * maybeBatch.ts:16-39; also BlsSingleThreadVerifier, singleThread.ts:14-36) */
+  BGV_MODE_PER_JOB = 1
+};
+
+/* Pubkey record formats for bgv_pubkeys_put. */
+enum { BGV_PK_COMPRESSED = 48, BGV_PK_UNCOMPRESSED = 96 };
+
+typedef struct bgv_ctx bgv_ctx;
+
+/* One signature set: ISignatureSet (state-transition/src/util/signatureSets.ts:5-22).
+ * single     -> n_pk = 1
+ * aggregate  -> n_pk = pubkeys.length (0 rejects with BGV_E_EMPTY_AGGREGATE)
+ * Pubkeys are trusted (already subgroup/infinity checked, interface.ts:33-36) and are
+ * given either as validator indices into the device cache (pk_indices) or, for keys
+ * not in the cache, as n_pk x 96-byte uncompressed records (pk_bytes, the
+ * SerializedSet.publicKey format of multithread/types.ts:8-12). */
+typedef struct {
+  uint32_t n_pk;
+  uint32_t sig_len;           /* length of sig as received; 96 is the only valid size */
+  const uint32_t* pk_indices; /* n_pk indices, or NULL */
+  const uint8_t* pk_bytes;    /* n_pk * 96 bytes when pk_indices is NULL */
+  const uint8_t* msg;         /* 32-byte signing root */
+  const uint8_t* sig;         /* compressed G2 signature, untrusted wire bytes */
+} bgv_set;
+
+/* One verifySignatureSets job (BlsWorkReq, multithread/types.ts:14-17): a
+ * contiguous run of sets and its VerifySignatureOpts.batchable flag. */
+typedef struct {
+  uint32_t first_set;
+  uint32_t n_sets;
+  uint32_t batchable;
+} bgv_job;
+
+/* Counters mirroring BlsWorkResult (multithread/types.ts:24-36) plus device timing. */
+typedef struct {
+  uint64_t batch_retries;      /* mixed-job device groups that failed and were retried per job */
+  uint64_t batch_sigs_success; /* sets verified valid in mixed-job groups */
+  uint64_t device_groups;      /* device groups launched (each one final exponentiation) */
+  uint64_t sets_verified;      /* slots launched, retries included */
+  double device_ms;            /* HIP-event time of the kernels of this call */
+  double wall_ms;              /* host wall time of the call */
+} bgv_stats;
+
+/* Create a context on the given HIP devices (NULL/0 = device 0).  Replaces the
+ * pool constructor, multithread/index.ts:114-132. */
+int bgv_init(const int* devices, int ndev, bgv_ctx** out);
+
+/* Release all device memory.  After bgv_close() every call returns BGV_E_CLOSED. */
+int bgv_close(bgv_ctx* ctx);
+int bgv_destroy(bgv_ctx* ctx);
+
+/* Upload validator pubkeys [first_index, first_index + n) into the device-resident
+ * cache (replicated on every device).  fmt = BGV_PK_COMPRESSED (48-byte ZCash, as in
+ * the beacon state) or BGV_PK_UNCOMPRESSED (96 bytes).  Keys are trusted: decoded
+ * without a subgroup check, as Index2PubkeyCache does
+ * (state-transition/src/cache/pubkeyCache.ts:56-77, epochContext.ts:702-705).
+ * Returns BGV_OK, or -code of the first undecodable key. */
+int bgv_pubkeys_put(bgv_ctx* ctx, uint32_t first_index, const uint8_t* keys, size_t n, int fmt);
+size_t bgv_pubkeys_count(const bgv_ctx* ctx);
+
+/* Verify njobs jobs over nsets sets; out_job_codes[j] receives 1, 0 or -error.
+ * Replaces BlsMultiThreadWorkerPool.verifySignatureSets + the worker's
+ * verifyManySignatureSets + verifySignatureSetsMaybeBatch
+ * (multithread/index.ts:134-174, worker.ts:32-108, maybeBatch.ts:16-39).
+ * stats may be NULL. */
+int bgv_verify(bgv_ctx* ctx, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
+               int32_t* out_job_codes, bgv_stats* stats);
+
+/* Asynchronous form for the N-API addon (napi_async_work): the call runs on the
+ * context's worker thread and `done(user, rc)` is invoked there when out_job_codes
+ * and stats are filled.  The caller keeps every buffer alive until then. */
+typedef void (*bgv_done_fn)(void* user, int rc);
+int bgv_verify_async(bgv_ctx* ctx, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
+                     int32_t* out_job_codes, bgv_stats* stats, bgv_done_fn done, void* user);
+
+/* Parity hook for bls.PublicKey.aggregate + toBytes(uncompressed)
+ * (chain/bls/utils.ts:5-16, multithread/index.ts:160): sum of cached pubkeys,
+ * 96-byte uncompressed ZCash encoding (0x40 flag for infinity). */
+int bgv_aggregate_pubkeys(bgv_ctx* ctx, const uint32_t* indices, size_t n, uint8_t out96[96]);
+
+/* Parity hook for hash_to_G2 with DST BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_:
+ * n messages (concatenated, lengths in lens) -> n x 192-byte uncompressed points
+ * (x.c1 | x.c0 | y.c1 | y.c0). */
+int bgv_hash_to_g2(bgv_ctx* ctx, const uint8_t* msgs, const uint32_t* lens, size_t n, uint8_t* out192);
+
+/* Bench/test utilities (not part of IBlsVerifier): derive public keys and sign on
+ * the device.  sks are n x 32-byte big-endian secret keys (SecretKey.fromBytes).
+ * bgv_keygen writes n x 48-byte compressed pubkeys to out48 (may be NULL) and, when
+ * cache_first >= 0, stores them in the pubkey cache at [cache_first, cache_first + n).
+ * bgv_sign writes n x 96-byte compressed signatures sk_i * H(msg_i) (msgs: n x 32 B). */
+int bgv_keygen(bgv_ctx* ctx, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48);
+int bgv_sign(bgv_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, size_t n, uint8_t* out96);
+
+/* Deterministic batch randomizers for tests (seed != 0: splitmix64 stream;
+ * seed == 0: getrandom(), the default). */
+int bgv_set_rng_seed(bgv_ctx* ctx, uint64_t seed);
+
+/* Per-kernel device time (HIP events between the kernels of each verify launch).
+ * Reads the accumulated milliseconds per kernel (kernel_ms[n], names[n], launches)
+ * and then, if enable >= 0, resets the counters and switches event recording on (1)
+ * or off (0).  Returns the number of kernels in a verify launch. */
+int bgv_profile(bgv_ctx* ctx, int enable, double* kernel_ms, const char** names, int n, uint64_t* launches);
+
+/* Human-readable name of a status code ("BLST_INVALID_SIZE", ...). */
+const char* bgv_strerror(int code);
+
+int bgv_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLSGPU_H */

@@ -1,0 +1,53 @@
+"""Build libblsgpu.so (HIP kernels for gfx950 + C-ABI host orchestration) in-tree.
+
+    python -m lodestar_amd.build [--force]
+
+The .so lands next to this file so it travels with the repository snapshot to
+the GPU box (git-ignored, not gpurun-ignored).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libblsgpu.so")
+SOURCES = [os.path.join(CSRC, "bgv_kernels.hip"), os.path.join(CSRC, "bgv_api.cpp")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("BGV_OFFLOAD_ARCH", "gfx950")
+
+
+def deps():
+    out = list(SOURCES) + [os.path.join(HERE, "..", "include", "blsgpu.h")]
+    out += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    return out
+
+
+def up_to_date(lib=LIB):
+    return os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(d) for d in deps())
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+               "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,369 @@
+// Batch BLS12-381 signature-set verification kernels for CDNA4 (gfx950).
+//
+// One signature set per lane.  A verify call runs these kernels in order on
+// one HIP stream (see bgv_api.cpp):
+//
+//   k_sig      decompress + subgroup-check the 96-byte signature, r_i * sig_i
+//   k_hash     hash_to_G2(signing root) -> affine H(m_i)
+//   k_pk       gather + aggregate pubkeys from the device cache, r_i * pk_i -> affine
+//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i))
+//   k_reduce   per device group (one wavefront): prod f_i and sum r_i sig_i via an LDS tree
+//   k_final    per group: f * MillerLoop(-G1, sum r_i sig_i) -> final exponentiation -> == 1
+//
+// This is the randomized batch equation of blst's verifyMultipleAggregateSignatures
+// (called from packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25):
+//   prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i) == 1.
+// A one-set group is the core verify of maybeBatch.ts:34-38 raised to the
+// power r (nonzero, < group order), which has the same verdict.
+#include "bgv_layout.h"
+#define BGV_KERNEL_SIDE 1
+#include "bls_hash.h"
+#include "bls_pairing.h"
+
+extern "C" {
+
+__global__ void __launch_bounds__(64) k_sig(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                            g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  g2_jac out = jac_infinity<fp2_t>();
+  if (d.flags & BGV_SLOT_PAD) {
+    st = BGV_ST_INFINITY;
+  } else if (d.sig_len != 96) {
+    st = BGV_INVALID_SIZE;
+  } else {
+    uint8_t b[96];
+    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
+    g2_aff a;
+    bool inf;
+    st = g2_decompress(&a, &inf, b);
+    if (st == BGV_OK) {
+      if (inf) {
+        st = BGV_ST_INFINITY;  // skipped in the accumulator, as blst does
+      } else {
+        const g2_jac j = jac_from_aff(a);
+        if (!g2_in_subgroup(j))
+          st = BGV_POINT_NOT_IN_GROUP;
+        else
+          out = jac_mul_u64(j, d.scalar);
+      }
+    }
+  }
+  rsig[s] = out;
+  sig_status[s] = st;
+}
+
+__global__ void __launch_bounds__(64) k_hash(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                             g2_aff* __restrict__ h) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  if (d.flags & BGV_SLOT_PAD) return;
+  uint8_t msg[32];
+  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
+  g2_aff a;
+  jac_to_aff(&a, hash_to_g2(msg, 32));
+  h[s] = a;
+}
+
+__global__ void __launch_bounds__(64) k_pk(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                           const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                           const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                           int32_t* __restrict__ pk_status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  if (d.flags & BGV_SLOT_PAD) {
+    pk_status[s] = BGV_ST_INFINITY;
+    return;
+  }
+  g1_jac acc = jac_infinity<fp_t>();
+  const bool cached = (d.flags & BGV_SLOT_PK_CACHED) != 0;
+  for (uint32_t k = 0; k < d.n_pk; ++k) {
+    g1_aff a;
+    if (cached) {
+      a = cache[pk_idx[d.pk_off + k]];
+    } else {
+      uint8_t b[96];
+      const uint8_t* src = pk_bytes + 96ull * (d.pk_off + k);
+      for (int i = 0; i < 96; ++i) b[i] = src[i];
+      bool inf;
+      const int rc = g1_deserialize(&a, &inf, b);
+      if (rc == BGV_OK && !inf && !g1_aff_on_curve(a)) st = BGV_POINT_NOT_ON_CURVE;
+      else if (rc != BGV_OK) st = rc;
+      if (st != BGV_OK) break;
+      if (inf) continue;
+    }
+    acc = jac_add_aff(acc, a);
+  }
+  if (st == BGV_OK) {
+    g1_aff out;
+    if (jac_to_aff(&out, jac_mul_u64(acc, d.scalar)))
+      rpk[s] = out;
+    else
+      st = BGV_ST_INFINITY;
+  }
+  pk_status[s] = st;
+}
+
+__global__ void __launch_bounds__(64) k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                               const g1_aff* __restrict__ rpk, const g2_aff* __restrict__ h,
+                                               const int32_t* __restrict__ sig_status,
+                                               const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const int32_t ss = sig_status[s];
+  const bool live = !(slots[s].flags & BGV_SLOT_PAD) && (ss == BGV_ST_OK || ss == BGV_ST_INFINITY) &&
+                    pk_status[s] == BGV_ST_OK;
+  fp12_t r = fp12_one();
+  if (live) r = miller_loop(rpk[s], h[s]);
+  f[s] = r;
+}
+
+// One wavefront per device group: LDS tree of Fp12 products and G2 sums.
+__global__ void __launch_bounds__(64) k_reduce(const bgv_dgroup* __restrict__ groups, const fp12_t* __restrict__ f,
+                                               const g2_jac* __restrict__ rsig,
+                                               const int32_t* __restrict__ sig_status,
+                                               const int32_t* __restrict__ pk_status, fp12_t* __restrict__ fg,
+                                               g2_jac* __restrict__ sg) {
+  extern __shared__ uint32_t lds[];
+  fp12_t* lf = reinterpret_cast<fp12_t*>(lds);
+  g2_jac* ls = reinterpret_cast<g2_jac*>(lds + BGV_WAVE * (sizeof(fp12_t) / 4));
+  const bgv_dgroup g = groups[blockIdx.x];
+  const uint32_t j = threadIdx.x;
+  fp12_t mf = fp12_one();
+  g2_jac ms = jac_infinity<fp2_t>();
+  if (j < g.n_slots) {
+    const uint32_t s = g.first_slot + j;
+    mf = f[s];
+    if (sig_status[s] == BGV_ST_OK && pk_status[s] == BGV_ST_OK) ms = rsig[s];
+  }
+  for (uint32_t d = 1; d < BGV_WAVE; d <<= 1) {
+    lf[j] = mf;
+    ls[j] = ms;
+    __syncthreads();
+    if ((j & (2 * d - 1)) == 0 && j + d < g.n_slots) {
+      mf = fp12_mul(mf, lf[j + d]);
+      ms = jac_add(ms, ls[j + d]);
+    }
+    __syncthreads();
+  }
+  if (j == 0) {
+    fg[blockIdx.x] = mf;
+    sg[blockIdx.x] = ms;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
+                                              const g2_jac* __restrict__ sg, int32_t* __restrict__ verdict) {
+  const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= ngroups) return;
+  fp12_t f = fg[gi];
+  g2_aff sa;
+  if (jac_to_aff(&sa, sg[gi])) f = fp12_mul(f, miller_loop(g1_neg_generator(), sa));
+  verdict[gi] = fp12_is_one(final_exp(f)) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Parity hooks (bgv_aggregate_pubkeys / bgv_hash_to_g2 in the C-ABI)
+// ---------------------------------------------------------------------------
+__global__ void k_aggregate_cached(const uint32_t* __restrict__ idx, uint32_t n, const g1_aff* __restrict__ cache,
+                                   uint8_t* __restrict__ out96) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  g1_jac acc = jac_infinity<fp_t>();
+  for (uint32_t k = 0; k < n; ++k) acc = jac_add_aff(acc, cache[idx[k]]);
+  g1_aff a;
+  const bool fin = jac_to_aff(&a, acc);
+  uint8_t b[96];
+  g1_serialize(b, a, !fin);
+  for (int i = 0; i < 96; ++i) out96[i] = b[i];
+}
+
+__global__ void k_hash_msgs(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ offs,
+                            const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ out192) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2_aff a;
+  const bool fin = jac_to_aff(&a, hash_to_g2(msgs + offs[i], lens[i]));
+  uint8_t b[192];
+  g2_serialize(b, a, !fin);
+  for (int k = 0; k < 192; ++k) out192[192ull * i + k] = b[k];
+}
+
+// 48-byte compressed pubkeys -> device cache entries (trusted, no subgroup check:
+// state-transition/src/cache/pubkeyCache.ts:75 decompresses without validation)
+__global__ void k_cache_put_compressed(const uint8_t* __restrict__ keys, uint32_t n, g1_aff* __restrict__ cache,
+                                       int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[48];
+  for (int k = 0; k < 48; ++k) b[k] = keys[48ull * i + k];
+  g1_aff a;
+  bool inf;
+  int rc = g1_decompress(&a, &inf, b);
+  if (rc == BGV_OK && inf) rc = BGV_PK_IS_INFINITY;
+  if (rc == BGV_OK) cache[i] = a;
+  status[i] = rc;
+}
+
+__global__ void k_cache_put_uncompressed(const uint8_t* __restrict__ keys, uint32_t n, g1_aff* __restrict__ cache,
+                                         int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[96];
+  for (int k = 0; k < 96; ++k) b[k] = keys[96ull * i + k];
+  g1_aff a;
+  bool inf;
+  int rc = g1_deserialize(&a, &inf, b);
+  if (rc == BGV_OK && inf) rc = BGV_PK_IS_INFINITY;
+  if (rc == BGV_OK && !g1_aff_on_curve(a)) rc = BGV_POINT_NOT_ON_CURVE;
+  if (rc == BGV_OK) cache[i] = a;
+  status[i] = rc;
+}
+
+
+// ---------------------------------------------------------------------------
+// Key generation and signing (bench / test data on the device; not on the
+// verify path).  Secret keys are 32-byte big-endian scalars < r
+// (SecretKey.fromBytes, state-transition/src/util/interop.ts:19-22).
+// ---------------------------------------------------------------------------
+__device__ static void sk_words(const uint8_t* be32, uint32_t k[8]) {
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* q = be32 + 28 - 4 * i;
+    k[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+__global__ void k_keygen(const uint8_t* __restrict__ sks, uint32_t n, g1_aff* __restrict__ cache,
+                         uint8_t* __restrict__ out48) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  sk_words(sks + 32ull * i, k);
+  g1_aff a;
+  const bool fin = jac_to_aff(&a, jac_mul_u256(jac_from_aff(g1_generator()), k));
+  if (cache) cache[i] = a;
+  if (out48) {
+    uint8_t b[48];
+    g1_compress(b, a, !fin);
+    for (int q = 0; q < 48; ++q) out48[48ull * i + q] = b[q];
+  }
+}
+
+__global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs, uint32_t n,
+                       uint8_t* __restrict__ out96) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  sk_words(sks + 32ull * i, k);
+  uint8_t m[32];
+  for (int q = 0; q < 32; ++q) m[q] = msgs[32ull * i + q];
+  g2_aff a;
+  const bool fin = jac_to_aff(&a, jac_mul_u256(hash_to_g2(m, 32), k));
+  uint8_t b[96];
+  g2_compress(b, a, !fin);
+  for (int q = 0; q < 96; ++q) out96[96ull * i + q] = b[q];
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (declared in bgv_launch.h; called from bgv_api.cpp)
+// ---------------------------------------------------------------------------
+#include "bgv_launch.h"
+
+static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
+
+hipError_t bgv_launch_verify(const bgv_dev_batch& b, hipStream_t st, hipEvent_t* ev) {
+  const uint32_t n = b.nslots;
+  if (n == 0) return hipSuccess;
+  // ev (optional): BGV_NKERNELS + 1 events bracketing each kernel, for per-kernel timing
+#define BGV_MARK(i) \
+  if (ev) (void)hipEventRecord(ev[i], st)
+  BGV_MARK(0);
+  hipLaunchKernelGGL(k_sig, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.rsig, b.sig_status);
+  BGV_MARK(1);
+  hipLaunchKernelGGL(k_hash, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.h);
+  BGV_MARK(2);
+  hipLaunchKernelGGL(k_pk, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.pk_idx,
+                     reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status);
+  BGV_MARK(3);
+  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.rpk, b.h, b.sig_status, b.pk_status,
+                     b.f);
+  BGV_MARK(4);
+  const size_t lds = BGV_WAVE * (sizeof(fp12_t) + sizeof(g2_jac));
+  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, st, b.groups, b.f, b.rsig, b.sig_status, b.pk_status,
+                     b.fg, b.sg);
+  BGV_MARK(5);
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.fg, b.sg, b.verdict);
+  BGV_MARK(6);
+#undef BGV_MARK
+  return hipGetLastError();
+}
+
+size_t bgv_slot_bytes() {
+  return sizeof(g2_jac) + sizeof(g2_aff) + sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
+}
+size_t bgv_group_bytes() { return sizeof(fp12_t) + sizeof(g2_jac) + sizeof(int32_t); }
+size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
+
+void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
+  uint8_t* p = static_cast<uint8_t*>(slot_mem);
+  b->rsig = reinterpret_cast<g2_jac*>(p);
+  p += sizeof(g2_jac) * (size_t)cap_slots;
+  b->h = reinterpret_cast<g2_aff*>(p);
+  p += sizeof(g2_aff) * (size_t)cap_slots;
+  b->rpk = reinterpret_cast<g1_aff*>(p);
+  p += sizeof(g1_aff) * (size_t)cap_slots;
+  b->f = reinterpret_cast<fp12_t*>(p);
+  p += sizeof(fp12_t) * (size_t)cap_slots;
+  b->sig_status = reinterpret_cast<int32_t*>(p);
+  p += sizeof(int32_t) * (size_t)cap_slots;
+  b->pk_status = reinterpret_cast<int32_t*>(p);
+  uint8_t* q = static_cast<uint8_t*>(group_mem);
+  b->fg = reinterpret_cast<fp12_t*>(q);
+  q += sizeof(fp12_t) * (size_t)cap_groups;
+  b->sg = reinterpret_cast<g2_jac*>(q);
+  q += sizeof(g2_jac) * (size_t)cap_groups;
+  b->verdict = reinterpret_cast<int32_t*>(q);
+}
+
+hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_cache_entry* cache, int32_t* status,
+                                hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  g1_aff* c = reinterpret_cast<g1_aff*>(cache);
+  if (fmt == 48)
+    hipLaunchKernelGGL(k_cache_put_compressed, dim3(nblk(n, 64)), dim3(64), 0, st, keys, n, c, status);
+  else
+    hipLaunchKernelGGL(k_cache_put_uncompressed, dim3(nblk(n, 64)), dim3(64), 0, st, keys, n, c, status);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_aggregate(const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache, uint8_t* out96,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(k_aggregate_cached, dim3(1), dim3(64), 0, st, idx, n, reinterpret_cast<const g1_aff*>(cache),
+                     out96);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_hash(const uint8_t* msgs, const uint32_t* offs, const uint32_t* lens, uint32_t n,
+                           uint8_t* out192, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hash_msgs, dim3(nblk(n, 64)), dim3(64), 0, st, msgs, offs, lens, n, out192);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_keygen, dim3(nblk(n, 64)), dim3(64), 0, st, sks, n, reinterpret_cast<g1_aff*>(cache), out48);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sign, dim3(nblk(n, 64)), dim3(64), 0, st, sks, msgs, n, out96);
+  return hipGetLastError();
+}

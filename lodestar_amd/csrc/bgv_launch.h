@@ -1,0 +1,58 @@
+// Internal interface between the HIP kernels (bgv_kernels.hip) and the host
+// orchestration (bgv_api.cpp).  Device pointers only; no torch types.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "bgv_layout.h"
+
+struct fp12_t;
+template <class F>
+struct jac_t;
+template <class F>
+struct aff_t;
+struct fp_t;
+struct fp2_t;
+
+// opaque cache entry (affine G1, Montgomery form)
+struct bgv_cache_entry;
+
+struct bgv_dev_batch {
+  uint32_t nslots, ngroups;
+  const bgv_dslot* slots;
+  const bgv_dgroup* groups;
+  const uint32_t* pk_idx;
+  const bgv_cache_entry* cache_opaque;
+  const uint8_t* pk_bytes;
+  // carved per-slot / per-group scratch
+  jac_t<fp2_t>* rsig;
+  aff_t<fp2_t>* h;
+  aff_t<fp_t>* rpk;
+  fp12_t* f;
+  int32_t* sig_status;
+  int32_t* pk_status;
+  fp12_t* fg;
+  jac_t<fp2_t>* sg;
+  int32_t* verdict;
+#ifdef BGV_KERNEL_SIDE
+  const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
+#endif
+};
+
+// kernels of one verify launch, in order (names for per-kernel timing)
+#define BGV_NKERNELS 6
+static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_sig", "k_hash", "k_pk", "k_miller", "k_reduce", "k_final"};
+hipError_t bgv_launch_verify(const bgv_dev_batch& b, hipStream_t st, hipEvent_t* ev);
+size_t bgv_slot_bytes();
+size_t bgv_group_bytes();
+size_t bgv_cache_entry_bytes();
+void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups);
+hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_cache_entry* cache, int32_t* status,
+                                hipStream_t st);
+hipError_t bgv_launch_aggregate(const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache, uint8_t* out96,
+                                hipStream_t st);
+hipError_t bgv_launch_hash(const uint8_t* msgs, const uint32_t* offs, const uint32_t* lens, uint32_t n,
+                           uint8_t* out192, hipStream_t st);
+hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st);
+hipError_t bgv_launch_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t st);

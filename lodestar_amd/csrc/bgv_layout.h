@@ -1,0 +1,41 @@
+// Device-side record layouts shared by the HIP kernels (bgv_kernels.hip) and
+// the host orchestration (bgv_api.cpp).  Plain C structs, no HIP types.
+//
+// A verify call is laid out as SLOTS: one lane per signature set.  Sets are
+// packed into device GROUPS of at most 64 slots that never straddle a 64-slot
+// (one wavefront) boundary, so a group's product/sum reduction is wave-local.
+// Padding slots (BGV_SLOT_PAD) are identity elements.
+#pragma once
+#include <stdint.h>
+
+#define BGV_WAVE 64
+
+enum {
+  BGV_SLOT_PAD = 1u,        // empty lane
+  BGV_SLOT_PK_CACHED = 2u,  // pubkeys are validator indices into the device cache
+  BGV_SLOT_PK_BYTES = 4u,   // pubkeys are 96-byte uncompressed records uploaded with the call
+};
+
+// Per-slot input record (160 B, 16-B aligned).
+struct bgv_dslot {
+  uint32_t flags;
+  uint32_t n_pk;    // pubkeys to aggregate (>= 1)
+  uint32_t pk_off;  // first index in the index array, or first 96-B record
+  uint32_t sig_len; // length of the signature bytes as received (96 is the only valid size)
+  uint64_t scalar;  // nonzero 64-bit batch randomizer r
+  uint32_t group;   // device group id
+  uint32_t pad_;
+  uint8_t msg[32];  // signing root
+  uint8_t sig[96];  // compressed G2 signature (untrusted wire bytes)
+};
+
+// Per-slot status codes written by the kernels (BLST numbering, see blsgpu.h)
+enum {
+  BGV_ST_OK = 0,
+  BGV_ST_INFINITY = 100,  // infinity signature / pubkey: valid encoding, skipped in the product
+};
+
+struct bgv_dgroup {
+  uint32_t first_slot;  // multiple of BGV_WAVE
+  uint32_t n_slots;     // 1..64
+};

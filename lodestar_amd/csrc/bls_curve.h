@@ -85,7 +85,7 @@ BGV_HD jac_t<F> jac_neg(const jac_t<F>& p) {
 
 // dbl-2009-l
 template <class F>
-BGV_HD jac_t<F> jac_dbl(const jac_t<F>& p) {
+BGV_NOINLINE jac_t<F> jac_dbl(const jac_t<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -125,7 +125,7 @@ BGV_HD jac_t<F> jac_add_raw(const jac_t<F>& p, const jac_t<F>& q, bool* h_zero, 
 
 // complete addition
 template <class F>
-BGV_HD jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
+BGV_NOINLINE jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
   bool hz, rz;
   jac_t<F> r = jac_add_raw(p, q, &hz, &rz);
   const bool pinf = jac_is_inf(p), qinf = jac_is_inf(q);
@@ -157,7 +157,7 @@ BGV_HD jac_t<F> jac_add_aff_raw(const jac_t<F>& p, const aff_t<F>& q, bool* h_ze
 }
 
 template <class F>
-BGV_HD jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
+BGV_NOINLINE jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
   bool hz, rz;
   jac_t<F> r = jac_add_aff_raw(p, q, &hz, &rz);
   const bool pinf = jac_is_inf(p);
@@ -168,7 +168,7 @@ BGV_HD jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
 
 // Jacobian -> affine; returns false for infinity (out untouched = zeros).
 template <class F>
-BGV_HD bool jac_to_aff(aff_t<F>* out, const jac_t<F>& p) {
+BGV_NOINLINE bool jac_to_aff(aff_t<F>* out, const jac_t<F>& p) {
   F zi = f_inv(p.z);
   F zi2 = f_sqr(zi);
   out->x = f_mul(p.x, zi2);
@@ -189,7 +189,7 @@ BGV_HD bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
 // with a 3-entry table; the add is computed in every lane and selected, so a
 // wave never diverges on scalar bits.
 template <class F>
-BGV_HD jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
+BGV_NOINLINE jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
   jac_t<F> t1 = p;
   jac_t<F> t2 = jac_dbl(p);
   jac_t<F> t3 = jac_add(t2, p);
@@ -205,9 +205,28 @@ BGV_HD jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
   return acc;
 }
 
+// [k]P for a 256-bit scalar given as 8 little-endian u32 words (secret keys in
+// the keygen/sign utilities), same 2-bit fixed window as jac_mul_u64.
+template <class F>
+BGV_NOINLINE jac_t<F> jac_mul_u256(const jac_t<F>& p, const uint32_t k[8]) {
+  jac_t<F> t1 = p;
+  jac_t<F> t2 = jac_dbl(p);
+  jac_t<F> t3 = jac_add(t2, p);
+  jac_t<F> acc = jac_infinity<F>();
+  BGV_NO_UNROLL for (int i = 254; i >= 0; i -= 2) {
+    acc = jac_dbl(jac_dbl(acc));
+    const uint32_t d = (k[i >> 5] >> (i & 31)) & 3u;
+    jac_t<F> s = jac_select(d == 2u, t1, t2);
+    s = jac_select(d == 3u, s, t3);
+    jac_t<F> sum = jac_add(acc, s);
+    acc = jac_select(d != 0u, acc, sum);
+  }
+  return acc;
+}
+
 // [|x|]P, |x| = 0xd201000000010000 (lane-uniform bits: no divergence)
 template <class F>
-BGV_HD jac_t<F> jac_mul_x_abs(const jac_t<F>& p) {
+BGV_NOINLINE jac_t<F> jac_mul_x_abs(const jac_t<F>& p) {
   jac_t<F> acc = p;
   const uint64_t X = BGV_X_ABS;
   BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {

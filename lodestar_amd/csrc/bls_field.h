@@ -1,10 +1,18 @@
 // BLS12-381 field tower for CDNA4 (gfx950): Fp, Fp2, Fp6, Fp12.
 //
-// One field element per lane: Fp = 12 x u32 limbs (little-endian) in Montgomery
-// form with R = 2^384, always fully reduced to [0, p).  Multiplication is
-// 12-limb CIOS whose inner step `(u64)a*b + t + c` lowers to v_mad_u64_u32
-// plus a 64-bit add (measured issue rate on MI355X: 16 lanes/clk/SIMD for the
-// mad, tools/ubench_valu.hip).
+// One field element per lane.  Fp is stored as 14 unsaturated 28-bit limbs
+// (one per u32, little-endian) in Montgomery form with R = 2^392.  Measured
+// on MI355X (tools/ubench_fpmul.hip): the row-wise 28-bit Montgomery product
+// lowers to 392 independent v_mad_u64_u32 with 64-bit accumulators and no
+// carry chains, and runs 1.7x faster than 12 x 32-bit CIOS (whose carries the
+// compiler splits into v_mov/v_lshl_add_u64 pairs).  v_mad_u64_u32 issues at
+// half rate (16 lanes/clk/SIMD), so the 28-bit product is mad-bound.
+//
+// Value invariant ("weakly reduced"): every fp_t holds normalized limbs
+// (< 2^28) and a value in [0, 2p).  fp_mul accepts inputs up to 4p with limbs
+// up to 2^29 (so a + b of two reduced values may feed it directly through
+// fp_add_nr) and returns a weakly reduced value: (ab + mp)/R < 16p^2/R + p < 2p.
+// Only comparisons and serialisation canonicalise to [0, p).
 //
 // Tower (same as blst / the IETF pairing draft):
 //   Fp2  = Fp[i]  / (i^2 + 1)
@@ -22,17 +30,35 @@
 #include <hip/hip_runtime.h>
 #define BGV_HD __host__ __device__ __forceinline__
 #define BGV_NOINLINE __host__ __device__ __noinline__
-#define BGV_CONST __constant__
 #else
 #define BGV_HD inline __attribute__((always_inline))
 #define BGV_NOINLINE __attribute__((noinline))
-#define BGV_CONST static const
+#endif
+
+// The Montgomery product is the only out-of-line primitive: ~560 instructions
+// per call, so the call is cheap, and keeping it out of line keeps kernels small
+// enough to compile in seconds rather than hours.
+#ifndef BGV_MUL_ATTR
+#define BGV_MUL_ATTR BGV_NOINLINE
 #endif
 
 #define BGV_UNROLL _Pragma("unroll")
 #define BGV_NO_UNROLL _Pragma("unroll 1")
 
-#define NL 12
+// Host-only op counting (tools/count_ops.py builds tests/native/hostsim.cpp with
+// -DBGV_COUNT_OPS to count Fp products per kernel for the roofline accounting).
+#if defined(BGV_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern "C" unsigned long long bgv_count_mul, bgv_count_sqr;
+#define BGV_COUNT_MUL() (++bgv_count_mul)
+#define BGV_COUNT_SQR() (++bgv_count_sqr)
+#else
+#define BGV_COUNT_MUL() ((void)0)
+#define BGV_COUNT_SQR() ((void)0)
+#endif
+
+#define NL 14
+#define LBITS 28
+#define LMASK 0x0fffffffu
 
 struct fp_t {
   uint32_t v[NL];
@@ -51,8 +77,11 @@ struct fp12_t {
 // Fp
 // ---------------------------------------------------------------------------
 BGV_HD uint32_t p_limb(int i) {
-  // p as an immediate table; indices are compile-time constants after unrolling
   const uint32_t P_[NL] = BGV_P_LIMBS;
+  return P_[i];
+}
+BGV_HD uint32_t p2_limb(int i) {
+  const uint32_t P_[NL] = BGV_2P_LIMBS;
   return P_[i];
 }
 
@@ -67,131 +96,179 @@ BGV_HD fp_t fp_one() {
   return r;
 }
 
-BGV_HD bool fp_is_zero(const fp_t& a) {
-  uint32_t acc = 0;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) acc |= a.v[i];
-  return acc == 0;
-}
-
-BGV_HD bool fp_eq(const fp_t& a, const fp_t& b) {
-  uint32_t acc = 0;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) acc |= a.v[i] ^ b.v[i];
-  return acc == 0;
-}
-
 // r = cond ? b : a   (branch-free select)
 BGV_HD fp_t fp_select(bool cond, const fp_t& a, const fp_t& b) {
   fp_t r;
-  uint32_t m = 0u - (uint32_t)cond;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = (a.v[i] & ~m) | (b.v[i] & m);
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = cond ? b.v[i] : a.v[i];
   return r;
 }
 
-// Reduce a value in [0, 2p) to [0, p).
-BGV_HD fp_t fp_reduce_once(const fp_t& a) {
+// a - 2p when a >= 2p (a normalized, a < 4p); result in [0, 2p).
+BGV_HD fp_t fp_reduce_2p(const fp_t& a) {
   fp_t d;
-  uint32_t borrow = 0;
+  int32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t s = (uint64_t)a.v[i] - p_limb(i) - borrow;
-    d.v[i] = (uint32_t)s;
-    borrow = (uint32_t)(s >> 63);
+    int32_t s = (int32_t)a.v[i] - (int32_t)p2_limb(i) + c;
+    d.v[i] = (uint32_t)s & LMASK;
+    c = s >> LBITS;  // arithmetic: -1 or 0
   }
-  return fp_select(borrow == 0, a, d);
+  return fp_select(c < 0, d, a);
+}
+
+// plain limb-wise sum, no carry and no reduction: only as an fp_mul/fp_sqr
+// operand (limbs < 2^29, value < 4p)
+BGV_HD fp_t fp_add_nr(const fp_t& a, const fp_t& b) {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i];
+  return r;
 }
 
 BGV_HD fp_t fp_add(const fp_t& a, const fp_t& b) {
   fp_t r;
   uint32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t s = (uint64_t)a.v[i] + b.v[i] + c;
-    r.v[i] = (uint32_t)s;
-    c = (uint32_t)(s >> 32);
+    uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & LMASK;
+    c = s >> LBITS;
   }
-  return fp_reduce_once(r);  // a + b < 2p < 2^382: no carry out of limb 11
+  return fp_reduce_2p(r);
 }
 
 BGV_HD fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
 
+// a - b + 2p, normalized, in (0, 4p): only as an fp_mul operand
+BGV_HD fp_t fp_sub_nr(const fp_t& a, const fp_t& b) {
+  fp_t r;
+  int32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    int32_t s = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)p2_limb(i) + c;
+    r.v[i] = (uint32_t)s & LMASK;
+    c = s >> LBITS;
+  }
+  return r;
+}
+
 BGV_HD fp_t fp_sub(const fp_t& a, const fp_t& b) {
-  fp_t r, s;
-  uint32_t borrow = 0;
+  // d = a - b; if negative add 2p
+  fp_t d, r;
+  int32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
-    r.v[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
+    int32_t s = (int32_t)a.v[i] - (int32_t)b.v[i] + c;
+    d.v[i] = (uint32_t)s & LMASK;
+    c = s >> LBITS;
   }
-  // if borrow: r += p
-  uint32_t m = 0u - borrow, c = 0;
+  const uint32_t m = (uint32_t)c;  // 0 or 0xffffffff
+  uint32_t k = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t t = (uint64_t)r.v[i] + (p_limb(i) & m) + c;
-    s.v[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
+    uint32_t s = d.v[i] + (p2_limb(i) & m) + k;
+    r.v[i] = s & LMASK;
+    k = s >> LBITS;
   }
-  return s;
+  return r;
 }
 
 BGV_HD fp_t fp_neg(const fp_t& a) {
+  // 2p - a in (0, 2p]; maps 0 to 0 so the result stays below 2p
   fp_t r;
-  uint32_t borrow = 0;
+  int32_t c = 0;
+  uint32_t nz = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t d = (uint64_t)p_limb(i) - a.v[i] - borrow;
-    r.v[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
+    int32_t s = (int32_t)p2_limb(i) - (int32_t)a.v[i] + c;
+    r.v[i] = (uint32_t)s & LMASK;
+    c = s >> LBITS;
+    nz |= a.v[i];
   }
-  // -0 = 0
-  return fp_select(fp_is_zero(a), r, a);
+  return fp_select(nz == 0, r, a);
 }
 
-// Montgomery multiplication, CIOS, 12 x 32-bit.
-BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) {
-  uint32_t t[NL + 2];
-  BGV_UNROLL for (int i = 0; i < NL + 2; ++i) t[i] = 0;
+// Montgomery product, row-wise over 28-bit limbs (R = 2^392).  Each of the 14
+// u64 accumulators receives at most 2 products per row (< 2^58 + 2^56) over
+// 14 rows plus carries: < 2^63, so no carry ever leaves an accumulator early.
+BGV_MUL_ATTR fp_t fp_mul(fp_t a, fp_t b) {
+  BGV_COUNT_MUL();
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  uint64_t t[NL];
+  BGV_UNROLL for (int j = 0; j < NL; ++j) t[j] = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t c = 0;
-    const uint32_t ai = a.v[i];
-    BGV_UNROLL for (int j = 0; j < NL; ++j) {
-      uint64_t s = (uint64_t)ai * b.v[j] + t[j] + c;
-      t[j] = (uint32_t)s;
-      c = s >> 32;
-    }
-    uint64_t s = (uint64_t)t[NL] + c;
-    t[NL] = (uint32_t)s;
-    t[NL + 1] = (uint32_t)(s >> 32);
-    const uint32_t m = t[0] * BGV_N0;
-    s = (uint64_t)m * p_limb(0) + t[0];
-    c = s >> 32;
-    BGV_UNROLL for (int j = 1; j < NL; ++j) {
-      s = (uint64_t)m * p_limb(j) + t[j] + c;
-      t[j - 1] = (uint32_t)s;
-      c = s >> 32;
-    }
-    s = (uint64_t)t[NL] + c;
-    t[NL - 1] = (uint32_t)s;
-    t[NL] = t[NL + 1] + (uint32_t)(s >> 32);
+    BGV_UNROLL for (int j = 0; j < NL; ++j) t[j] += (uint64_t)a.v[i] * b.v[j];
+    const uint32_t m = ((uint32_t)t[0] * BGV_N0) & LMASK;
+    BGV_UNROLL for (int j = 0; j < NL; ++j) t[j] += (uint64_t)m * P_[j];
+    const uint64_t c = t[0] >> LBITS;
+    BGV_UNROLL for (int j = 0; j < NL - 1; ++j) t[j] = t[j + 1];
+    t[NL - 1] = 0;
+    t[0] += c;
   }
   fp_t r;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = t[i];
-  return fp_reduce_once(r);  // t < 2p since 4p < 2^384
+  BGV_UNROLL for (int j = 0; j < NL - 1; ++j) {
+    r.v[j] = (uint32_t)t[j] & LMASK;
+    t[j + 1] += t[j] >> LBITS;
+  }
+  r.v[NL - 1] = (uint32_t)t[NL - 1];
+  return r;
 }
 
-BGV_HD fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
+// Montgomery square: 105 products (cross terms doubled) then 14 reduction rows.
+BGV_MUL_ATTR fp_t fp_sqr(fp_t a) {
+  BGV_COUNT_SQR();
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int j = 0; j < 2 * NL; ++j) t[j] = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    t[2 * i] += (uint64_t)a.v[i] * a.v[i];
+    const uint32_t a2 = a.v[i] << 1;
+    BGV_UNROLL for (int j = i + 1; j < NL; ++j) t[i + j] += (uint64_t)a2 * a.v[j];
+  }
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    const uint32_t m = ((uint32_t)t[i] * BGV_N0) & LMASK;
+    BGV_UNROLL for (int j = 0; j < NL; ++j) t[i + j] += (uint64_t)m * P_[j];
+    t[i + 1] += t[i] >> LBITS;
+  }
+  fp_t r;
+  BGV_UNROLL for (int j = 0; j < NL - 1; ++j) {
+    r.v[j] = (uint32_t)t[NL + j] & LMASK;
+    t[NL + j + 1] += t[NL + j] >> LBITS;
+  }
+  r.v[NL - 1] = (uint32_t)t[2 * NL - 1];
+  return r;
+}
 
-// to / from Montgomery form (raw integers < p)
+// canonical representative in [0, p) of a weakly reduced value
+BGV_HD fp_t fp_canon(const fp_t& a) {
+  fp_t d;
+  int32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    int32_t s = (int32_t)a.v[i] - (int32_t)p_limb(i) + c;
+    d.v[i] = (uint32_t)s & LMASK;
+    c = s >> LBITS;
+  }
+  return fp_select(c < 0, d, a);
+}
+
+BGV_HD bool fp_is_zero(const fp_t& a) {
+  const fp_t c = fp_canon(a);
+  uint32_t acc = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) acc |= c.v[i];
+  return acc == 0;
+}
+
+BGV_HD bool fp_eq(const fp_t& a, const fp_t& b) { return fp_is_zero(fp_sub(a, b)); }
+
+// to / from Montgomery form (raw integers < 2^392)
 BGV_HD fp_t fp_to_mont(const fp_t& a) {
   const fp_t r2 = {BGV_R2};
   return fp_mul(a, r2);
 }
 
+// canonical raw integer in [0, p)
 BGV_HD fp_t fp_from_mont(const fp_t& a) {
-  fp_t one = fp_zero();
-  one.v[0] = 1;
-  return fp_mul(a, one);
+  const fp_t one = {BGV_RAW_ONE};
+  return fp_canon(fp_mul(a, one));
 }
 
-// a^e for a fixed (lane-uniform) exponent given as NL little-endian limbs.
-BGV_HD fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
-  fp_t r = fp_one();
-  BGV_NO_UNROLL for (int i = nbits - 1; i >= 0; --i) {
+// a^e for a fixed (lane-uniform) exponent given as 32-bit little-endian words.
+BGV_HD fp_t fp_pow_words(const fp_t& a, const uint32_t* e, int nbits) {
+  fp_t r = a;  // the top bit of every exponent used here is 1
+  BGV_NO_UNROLL for (int i = nbits - 2; i >= 0; --i) {
     r = fp_sqr(r);
     if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
   }
@@ -199,59 +276,58 @@ BGV_HD fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
 }
 
 BGV_HD fp_t fp_inv(const fp_t& a) {
-  const uint32_t e[NL] = BGV_EXP_P_MINUS_2;
-  return fp_pow_limbs(a, e, 381);
+  const uint32_t e[12] = BGV_EXP_P_MINUS_2;
+  return fp_pow_words(a, e, 381);
 }
 
 // a^((p-3)/4): for a QR, a * t = sqrt(a) and t = 1/sqrt(a).
 BGV_HD fp_t fp_pow_p_minus_3_div_4(const fp_t& a) {
-  const uint32_t e[NL] = BGV_EXP_P_MINUS_3_DIV_4;
-  return fp_pow_limbs(a, e, 379);
+  const uint32_t e[12] = BGV_EXP_P_MINUS_3_DIV_4;
+  return fp_pow_words(a, e, 379);
 }
 
 // sqrt candidate; returns true iff a is a square (then *out = a^((p+1)/4)).
 BGV_HD bool fp_sqrt(fp_t* out, const fp_t& a) {
-  const uint32_t e[NL] = BGV_EXP_P_PLUS_1_DIV_4;
-  fp_t s = fp_pow_limbs(a, e, 379);
+  const uint32_t e[12] = BGV_EXP_P_PLUS_1_DIV_4;
+  fp_t s = fp_pow_words(a, e, 379);
   *out = s;
   return fp_eq(fp_sqr(s), a);
 }
 
-// a / 2 mod p
+// a / 2 mod p (a weakly reduced; the limb-0 parity is the value's parity)
 BGV_HD fp_t fp_half(const fp_t& a) {
-  uint32_t m = 0u - (a.v[0] & 1);
+  const uint32_t m = 0u - (a.v[0] & 1);
   fp_t t;
   uint32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t s = (uint64_t)a.v[i] + (p_limb(i) & m) + c;
-    t.v[i] = (uint32_t)s;
-    c = (uint32_t)(s >> 32);
+    uint32_t s = a.v[i] + (p_limb(i) & m) + c;
+    t.v[i] = s & LMASK;
+    c = s >> LBITS;
   }
   fp_t r;
-  BGV_UNROLL for (int i = 0; i < NL - 1; ++i) r.v[i] = (t.v[i] >> 1) | (t.v[i + 1] << 31);
-  r.v[NL - 1] = (t.v[NL - 1] >> 1) | (c << 31);
-  return r;
+  BGV_UNROLL for (int i = 0; i < NL - 1; ++i) r.v[i] = (t.v[i] >> 1) | ((t.v[i + 1] & 1) << (LBITS - 1));
+  r.v[NL - 1] = t.v[NL - 1] >> 1;
+  return r;  // (a + p) / 2 < 1.5p
 }
 
-// Compare raw (non-Montgomery) integers: a > b
+// Compare canonical raw integers: a > b
 BGV_HD bool fp_raw_gt(const fp_t& a, const fp_t& b) {
-  // b - a borrows iff a > b
-  uint32_t borrow = 0;
+  int32_t c = 0;  // b - a borrows iff a > b
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t d = (uint64_t)b.v[i] - a.v[i] - borrow;
-    borrow = (uint32_t)(d >> 63);
+    int32_t s = (int32_t)b.v[i] - (int32_t)a.v[i] + c;
+    c = s >> LBITS;
   }
-  return borrow != 0;
+  return c < 0;
 }
 
 // raw integer < p ?
 BGV_HD bool fp_raw_lt_p(const fp_t& a) {
-  uint32_t borrow = 0;
+  int32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint64_t d = (uint64_t)a.v[i] - p_limb(i) - borrow;
-    borrow = (uint32_t)(d >> 63);
+    int32_t s = (int32_t)a.v[i] - (int32_t)p_limb(i) + c;
+    c = s >> LBITS;
   }
-  return borrow != 0;
+  return c < 0;
 }
 
 // ZCash "lexicographically largest": raw(a) > (p-1)/2
@@ -260,23 +336,31 @@ BGV_HD bool fp_lex_largest(const fp_t& a_mont) {
   return fp_raw_gt(fp_from_mont(a_mont), half);
 }
 
+// bits [lo, lo+28) of a big-endian byte string of n bytes (bits past the top read 0)
+BGV_HD uint32_t be_bits28(const uint8_t* b, int n, int lo) {
+  uint32_t r = 0;
+  BGV_UNROLL for (int k = 0; k < 5; ++k) {  // 28 bits touch at most 5 bytes
+    const int bytepos = (lo >> 3) + k;     // byte index from the little end
+    if (bytepos < n) r |= (uint32_t)((uint64_t)b[n - 1 - bytepos] << (8 * k) >> (lo & 7));
+  }
+  return r & LMASK;
+}
+
 // big-endian 48 bytes -> raw limbs
 BGV_HD fp_t fp_from_be48(const uint8_t* b) {
   fp_t r;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    const uint8_t* q = b + 44 - 4 * i;
-    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-  }
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = be_bits28(b, 48, LBITS * i);
   return r;
 }
 
+// canonical raw limbs -> big-endian 48 bytes
 BGV_HD void fp_to_be48(uint8_t* b, const fp_t& raw) {
-  BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    uint8_t* q = b + 44 - 4 * i;
-    q[0] = (uint8_t)(raw.v[i] >> 24);
-    q[1] = (uint8_t)(raw.v[i] >> 16);
-    q[2] = (uint8_t)(raw.v[i] >> 8);
-    q[3] = (uint8_t)raw.v[i];
+  BGV_UNROLL for (int k = 0; k < 48; ++k) {
+    const int bit = 8 * k;  // byte k from the little end
+    const int li = bit / LBITS, sh = bit % LBITS;
+    uint32_t v = raw.v[li] >> sh;
+    if (sh > LBITS - 8 && li + 1 < NL) v |= raw.v[li + 1] << (LBITS - sh);
+    b[47 - k] = (uint8_t)v;
   }
 }
 
@@ -296,14 +380,14 @@ BGV_HD fp2_t fp2_dbl(const fp2_t& a) { return fp2_t{fp_dbl(a.c0), fp_dbl(a.c1)};
 BGV_HD fp2_t fp2_neg(const fp2_t& a) { return fp2_t{fp_neg(a.c0), fp_neg(a.c1)}; }
 BGV_HD fp2_t fp2_conj(const fp2_t& a) { return fp2_t{a.c0, fp_neg(a.c1)}; }
 
-BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+BGV_NOINLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   fp_t t0 = fp_mul(a.c0, b.c0);
   fp_t t1 = fp_mul(a.c1, b.c1);
   fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return fp2_t{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
-BGV_HD fp2_t fp2_sqr(const fp2_t& a) {
+BGV_NOINLINE fp2_t fp2_sqr(const fp2_t& a) {
   fp_t t = fp_mul(a.c0, a.c1);
   return fp2_t{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
 }
@@ -313,7 +397,7 @@ BGV_HD fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { return fp2_t{fp_mul(a.c
 // multiply by xi = 1 + i
 BGV_HD fp2_t fp2_mul_xi(const fp2_t& a) { return fp2_t{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 
-BGV_HD fp2_t fp2_inv(const fp2_t& a) {
+BGV_NOINLINE fp2_t fp2_inv(const fp2_t& a) {
   fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp_t ni = fp_inv(n);
   return fp2_t{fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
@@ -324,7 +408,7 @@ BGV_HD fp2_t fp2_half(const fp2_t& a) { return fp2_t{fp_half(a.c0), fp_half(a.c1
 // Square root in Fp2 (p = 3 mod 4) by the norm ("complex") method with one
 // shared exponentiation for sqrt and inverse.  Returns false if a is not a
 // square.  Any root is returned; callers fix the sign.
-BGV_HD bool fp2_sqrt(fp2_t* out, const fp2_t& a) {
+BGV_NOINLINE bool fp2_sqrt(fp2_t* out, const fp2_t& a) {
   const fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp_t g;
   const bool n_sq = fp_sqrt(&g, n);
@@ -372,7 +456,7 @@ BGV_HD fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) {
 BGV_HD fp6_t fp6_neg(const fp6_t& a) { return fp6_t{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 BGV_HD fp6_t fp6_mul_v(const fp6_t& a) { return fp6_t{fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
-BGV_HD fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
+BGV_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
   fp2_t t0 = fp2_mul(a.c0, b.c0);
   fp2_t t1 = fp2_mul(a.c1, b.c1);
   fp2_t t2 = fp2_mul(a.c2, b.c2);
@@ -382,7 +466,7 @@ BGV_HD fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
   return fp6_t{c0, c1, c2};
 }
 
-BGV_HD fp6_t fp6_sqr(const fp6_t& a) {
+BGV_NOINLINE fp6_t fp6_sqr(const fp6_t& a) {
   // CH-SQR2
   fp2_t s0 = fp2_sqr(a.c0);
   fp2_t ab = fp2_mul(a.c0, a.c1);
@@ -398,7 +482,7 @@ BGV_HD fp6_t fp6_sqr(const fp6_t& a) {
 }
 
 // a * (b0 + b1 v)
-BGV_HD fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
+BGV_NOINLINE fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
   fp2_t t0 = fp2_mul(a.c0, b0);
   fp2_t t1 = fp2_mul(a.c1, b1);
   fp2_t c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), t0);
@@ -412,7 +496,7 @@ BGV_HD fp6_t fp6_mul_1(const fp6_t& a, const fp2_t& b1) {
   return fp6_t{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
 }
 
-BGV_HD fp6_t fp6_inv(const fp6_t& a) {
+BGV_NOINLINE fp6_t fp6_inv(const fp6_t& a) {
   fp2_t t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   fp2_t t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   fp2_t t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -437,7 +521,7 @@ BGV_HD bool fp12_is_one(const fp12_t& a) {
 
 BGV_HD fp12_t fp12_conj(const fp12_t& a) { return fp12_t{a.c0, fp6_neg(a.c1)}; }
 
-BGV_HD fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
+BGV_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
   fp6_t t0 = fp6_mul(a.c0, b.c0);
   fp6_t t1 = fp6_mul(a.c1, b.c1);
   fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
@@ -445,7 +529,7 @@ BGV_HD fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
   return fp12_t{c0, c1};
 }
 
-BGV_HD fp12_t fp12_sqr(const fp12_t& a) {
+BGV_NOINLINE fp12_t fp12_sqr(const fp12_t& a) {
   fp6_t t = fp6_mul(a.c0, a.c1);
   fp6_t s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   fp6_t c0 = fp6_sub(fp6_sub(s, t), fp6_mul_v(t));
@@ -454,7 +538,7 @@ BGV_HD fp12_t fp12_sqr(const fp12_t& a) {
 
 // f * (l0 + l1 w^2 + l3 w^3): a line with nonzero tower coefficients
 // c0.c0 = l0, c0.c1 = l1, c1.c1 = l3.
-BGV_HD fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+BGV_NOINLINE fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
   fp6_t t0 = fp6_mul_01(f.c0, l0, l1);
   fp6_t t1 = fp6_mul_1(f.c1, l3);
   fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l3)), t0), t1);
@@ -462,13 +546,13 @@ BGV_HD fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, c
   return fp12_t{c0, c1};
 }
 
-BGV_HD fp12_t fp12_inv(const fp12_t& a) {
+BGV_NOINLINE fp12_t fp12_inv(const fp12_t& a) {
   fp6_t n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
   fp6_t ni = fp6_inv(n);
   return fp12_t{fp6_mul(a.c0, ni), fp6_neg(fp6_mul(a.c1, ni))};
 }
 
-BGV_HD fp12_t fp12_frob(const fp12_t& a) {
+BGV_NOINLINE fp12_t fp12_frob(const fp12_t& a) {
   const fp2_t g[6] = BGV_FROB1;
   fp12_t r;
   r.c0.c0 = fp2_conj(a.c0.c0);
@@ -500,7 +584,7 @@ BGV_HD void fp4_sqr(fp2_t* c0, fp2_t* c1, const fp2_t& a, const fp2_t& b) {
   *c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
 }
 
-BGV_HD fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
+BGV_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
   fp2_t z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2;
   fp2_t z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   fp2_t t0, t1, t2, t3;

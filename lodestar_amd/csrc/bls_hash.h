@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 BGV_HD uint32_t sha_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-BGV_HD void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
+BGV_NOINLINE void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
   const uint32_t K[64] = {
       0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
       0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
@@ -78,7 +78,7 @@ BGV_HD void sha256_virtual(uint32_t out[8], const G& get, uint32_t total_len) {
   sha256_init(st);
   const uint32_t padded = ((total_len + 9 + 63) / 64) * 64;
   const uint64_t bitlen = (uint64_t)total_len * 8;
-  BGV_UNROLL for (uint32_t base = 0; base < padded; base += 64) {
+  BGV_NO_UNROLL for (uint32_t base = 0; base < padded; base += 64) {
     uint32_t blk[16];
     BGV_UNROLL for (int wi = 0; wi < 16; ++wi) {
       uint32_t word = 0;
@@ -155,12 +155,21 @@ BGV_HD void expand_message_xmd_256(uint32_t ub[64], const uint8_t* msg, uint32_t
   }
 }
 
-// 64 big-endian bytes (as 16 words) -> Fp (Montgomery), reduced mod p
+// bits [lo, lo+28) of a big-endian string of 16 u32 words (64 bytes)
+BGV_HD uint32_t be_words_bits28(const uint32_t* w, int lo) {
+  const int wi = lo >> 5, sh = lo & 31;  // word index from the little end
+  uint64_t v = w[15 - wi];
+  if (wi + 1 < 16) v |= (uint64_t)w[14 - wi] << 32;
+  return (uint32_t)(v >> sh) & LMASK;
+}
+
+// 64 big-endian bytes (as 16 words) -> Fp (Montgomery), reduced mod p:
+// value = hi * 2^392 + lo  ->  lo * R + hi * R^2 = mont(lo, R^2) + mont(hi, R^3)
 BGV_HD fp_t fp_from_be64_words(const uint32_t* w) {
-  // value = hi * 2^384 + lo, hi = words 0..3 (128 bits), lo = words 4..15 (384 bits)
   fp_t lo, hi = fp_zero();
-  BGV_UNROLL for (int i = 0; i < NL; ++i) lo.v[i] = w[15 - i];
-  BGV_UNROLL for (int i = 0; i < 4; ++i) hi.v[i] = w[3 - i];
+  BGV_UNROLL for (int i = 0; i < NL; ++i) lo.v[i] = be_words_bits28(w, LBITS * i);
+  BGV_UNROLL for (int i = 0; i < 5; ++i) hi.v[i] = be_words_bits28(w, 392 + LBITS * i);
+  hi.v[4] &= (1u << (512 - 392 - 4 * LBITS)) - 1;
   const fp_t r2 = {BGV_R2}, r3 = {BGV_R3};
   return fp_add(fp_mul(lo, r2), fp_mul(hi, r3));
 }
@@ -182,7 +191,7 @@ BGV_HD fp_t fp_sqrt_minus5() { return fp_t{BGV_SQRT_M5}; }
 
 // If g is a square in Fp2: *y = sqrt(g), returns true.  Otherwise *y = sqrt(Z g).
 // Two Fp exponentiations total (norm root + the Fp2 root).
-BGV_HD bool fp2_sqrt_or_z(fp2_t* y, const fp2_t& g, const fp_t& sqrt_m5) {
+BGV_NOINLINE bool fp2_sqrt_or_z(fp2_t* y, const fp2_t& g, const fp_t& sqrt_m5) {
   const fp2_t Z = BGV_SSWU_Z;
   const fp_t n = fp_add(fp_sqr(g.c0), fp_sqr(g.c1));
   const fp_t e = fp_pow_p_minus_3_div_4(n);
@@ -204,7 +213,7 @@ BGV_HD bool fp2_sqrt_or_z(fp2_t* y, const fp2_t& g, const fp_t& sqrt_m5) {
 }
 
 // returns the SWU point on E2' in affine coordinates
-BGV_HD void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
+BGV_NOINLINE void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
   const fp2_t A = BGV_SSWU_A, B = BGV_SSWU_B, Z = BGV_SSWU_Z;
   const fp2_t bza = BGV_SSWU_B_OVER_ZA, mba = BGV_SSWU_MINUS_B_OVER_A;
   fp2_t u2 = fp2_sqr(u);
@@ -227,7 +236,7 @@ BGV_HD void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
 }
 
 // 3-isogeny E2' -> E2 (RFC 9380 E.3), output Jacobian without inversion.
-BGV_HD g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
+BGV_NOINLINE g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
   const fp2_t xnum[4] = BGV_ISO_XNUM;
   const fp2_t xden[2] = BGV_ISO_XDEN;
   const fp2_t ynum[4] = BGV_ISO_YNUM;
@@ -246,7 +255,7 @@ BGV_HD g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
 }
 
 // Full hash_to_G2 of one message: returns Jacobian point in G2.
-BGV_HD g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
+BGV_NOINLINE g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, len);
   const fp_t sm5 = fp_sqrt_minus5();

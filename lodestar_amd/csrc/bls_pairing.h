@@ -8,7 +8,7 @@
 // Doubling step: T <- 2T; returns the tangent line at T evaluated at P,
 // scaled by Fp2/Fp4 factors that the final exponentiation kills:
 //   l0 = 3X^3 - 2Y^2,  l1 = -3X^2 Z^2 xP,  l3 = Z3 Z^2 yP
-BGV_HD void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const fp_t& xp_neg, const fp_t& yp) {
+BGV_NOINLINE void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const fp_t& xp_neg, const fp_t& yp) {
   fp2_t A = fp2_sqr(t.x);
   fp2_t B = fp2_sqr(t.y);
   fp2_t C = fp2_sqr(B);
@@ -29,7 +29,7 @@ BGV_HD void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const fp_t& x
 
 // Addition step: T <- T + Q (Q affine); returns the chord line at P:
 //   l0 = r xQ - yQ Z3,  l1 = -r xP,  l3 = Z3 yP   (r = 2(S2 - Y))
-BGV_HD void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const g2_aff& q, const fp_t& xp_neg,
+BGV_NOINLINE void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const g2_aff& q, const fp_t& xp_neg,
                        const fp_t& yp) {
   fp2_t ZZ = fp2_sqr(t.z);
   fp2_t U2 = fp2_mul(q.x, ZZ);
@@ -53,7 +53,7 @@ BGV_HD void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const g2_aff&
 
 // f_{|x|,Q}(P), conjugated for x < 0.  P = (xP, yP) in G1, Q in G2, both affine
 // and not infinity.  Loop over the bits of |x| = 0xd201000000010000 below the top.
-BGV_HD fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
+BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
   const fp_t xp_neg = fp_neg(p.x);
   const fp_t yp = p.y;
   g2_jac t = jac_from_aff(q);
@@ -77,7 +77,7 @@ BGV_HD fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
 }
 
 // a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
-BGV_HD fp12_t cyclotomic_pow_x(const fp12_t& a) {
+BGV_NOINLINE fp12_t cyclotomic_pow_x(const fp12_t& a) {
   const uint64_t X = BGV_X_ABS;
   fp12_t r = a;
   BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {
@@ -88,7 +88,7 @@ BGV_HD fp12_t cyclotomic_pow_x(const fp12_t& a) {
 }
 
 // f^(3 (p^12 - 1) / r) using 3 (p^4 - p^2 + 1)/r = (x-1)^2 (x+p) (x^2+p^2-1) + 3
-BGV_HD fp12_t final_exp(const fp12_t& f) {
+BGV_NOINLINE fp12_t final_exp(const fp12_t& f) {
   // easy part: f^((p^6 - 1)(p^2 + 1))
   fp12_t t = fp12_mul(fp12_conj(f), fp12_inv(f));
   t = fp12_mul(fp12_frob2(t), t);

@@ -39,6 +39,42 @@ static void out_g1(uint8_t* be, const g1_aff& a) {
 }
 
 extern "C" {
+#ifdef BGV_COUNT_OPS
+unsigned long long bgv_count_mul = 0, bgv_count_sqr = 0;
+void hs_count_reset() { bgv_count_mul = bgv_count_sqr = 0; }
+unsigned long long hs_count_mul() { return bgv_count_mul; }
+unsigned long long hs_count_sqr() { return bgv_count_sqr; }
+// per-lane bodies of the verify kernels (bgv_kernels.hip), for counting only
+int hs_k_sig_body(const uint8_t* sig96, uint64_t r) {
+  g2_aff a;
+  bool inf;
+  if (g2_decompress(&a, &inf, sig96) || inf) return 0;
+  const g2_jac j = jac_from_aff(a);
+  if (!g2_in_subgroup(j)) return 0;
+  g2_jac o = jac_mul_u64(j, r);
+  return !jac_is_inf(o);
+}
+int hs_k_hash_body(const uint8_t* msg32) {
+  g2_aff a;
+  return jac_to_aff(&a, hash_to_g2(msg32, 32));
+}
+int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
+  g1_aff p = in_g1(pk_aff_tl);
+  g1_jac acc = jac_infinity<fp_t>();
+  for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
+  g1_aff o;
+  return jac_to_aff(&o, jac_mul_u64(acc, r));
+}
+void hs_k_miller_body(const uint8_t* p, const uint8_t* q) { (void)miller_loop(in_g1(p), in_g2(q)); }
+void hs_k_final_body(const uint8_t* f, const uint8_t* s_aff) {
+  fp12_t x = fp12_mul(in_fp12(f), miller_loop(g1_neg_generator(), in_g2(s_aff)));
+  (void)fp12_is_one(final_exp(x));
+}
+void hs_k_reduce_step(const uint8_t* f, const uint8_t* s_aff) {
+  (void)fp12_mul(in_fp12(f), in_fp12(f));
+  (void)jac_add(jac_from_aff(in_g2(s_aff)), jac_dbl(jac_from_aff(in_g2(s_aff))));
+}
+#endif
 
 void hs_fp_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_mul(in_fp(a), in_fp(b))); }
 void hs_fp_add(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_add(in_fp(a), in_fp(b))); }
