@@ -22,6 +22,8 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <shared_mutex>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -30,15 +32,11 @@
 
 namespace {
 
-struct Device {
-  int id = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  hipEvent_t kev[BGV_NKERNELS + 1] = {};
-  // pubkey cache (replicated)
-  bgv_cache_entry* cache = nullptr;
-  size_t cache_cap = 0;
-  // per-call buffers, grown on demand
+// One in-flight verify call on one device: its own streams, events and buffers.
+struct Exec {
+  hipStream_t main = nullptr, aux[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr}, ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t kev[2 * BGV_NKERNELS] = {};
   void* slot_mem = nullptr;
   uint32_t slot_cap = 0;
   void* group_mem = nullptr;
@@ -49,8 +47,15 @@ struct Device {
   size_t idx_cap = 0;
   uint8_t* d_pkb = nullptr;
   size_t pkb_cap = 0;
-  int32_t* d_tmp = nullptr;
-  size_t tmp_cap = 0;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;  // utility work (cache upload, hooks, keygen)
+  bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
+  size_t cache_cap = 0;
+  std::vector<Exec*> free_execs;
+  std::vector<Exec*> all_execs;
 };
 
 struct Job {  // one async request
@@ -67,29 +72,35 @@ struct Job {  // one async request
 
 }  // namespace
 
+// concurrent verify calls per device (each on its own streams and buffers)
+#define BGV_EXECS_PER_DEVICE 8
+
 struct bgv_ctx {
   std::vector<Device> devs;
   size_t n_pubkeys = 0;
-  bool closed = false;
+  std::atomic<bool> closed{false};
+  std::mutex rng_mu;
   uint64_t rng_seed = 0, rng_state = 0;
+  std::shared_mutex cache_mu;  // verify: shared; cache writes: exclusive
+  std::mutex util_mu;          // utility streams
+  std::mutex exec_mu;
+  std::condition_variable exec_cv;
+  size_t rr = 0;  // round-robin device for the next call
+  std::mutex prof_mu;
   bool profile = false;
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
-  std::mutex mu;  // serialises device work
-  // host staging (pinned)
-  bgv_dslot* h_slots = nullptr;
-  size_t h_slots_cap = 0;
-  // async worker
-  std::thread worker;
+  // async workers
+  std::vector<std::thread> workers;
   std::mutex qmu;
   std::condition_variable qcv;
   std::deque<Job> queue;
   bool stop = false;
 };
 
-#define HIPCHK(x)                            \
-  do {                                       \
-    hipError_t e_ = (x);                     \
+#define HIPCHK(x)                               \
+  do {                                          \
+    hipError_t e_ = (x);                        \
     if (e_ != hipSuccess) return -BGV_E_DEVICE; \
   } while (0)
 
@@ -102,14 +113,17 @@ static uint64_t splitmix64(uint64_t* s) {
 
 // nonzero 64-bit randomizers (blst mul_n_aggregate with 64 random bits)
 static void fill_scalars(bgv_ctx* c, uint64_t* out, size_t n) {
-  if (c->rng_seed) {
-    for (size_t i = 0; i < n; ++i) {
-      uint64_t v;
-      do v = splitmix64(&c->rng_state);
-      while (v == 0);
-      out[i] = v;
+  {
+    std::lock_guard<std::mutex> lk(c->rng_mu);
+    if (c->rng_seed) {
+      for (size_t i = 0; i < n; ++i) {
+        uint64_t v;
+        do v = splitmix64(&c->rng_state);
+        while (v == 0);
+        out[i] = v;
+      }
+      return;
     }
-    return;
   }
   size_t got = 0;
   while (got < n * 8) {
@@ -131,32 +145,84 @@ static int grow(T** p, size_t* cap, size_t want) {
   return BGV_OK;
 }
 
-static int ensure_device_capacity(Device& d, uint32_t slots, uint32_t groups, size_t nidx, size_t npkb) {
-  HIPCHK(hipSetDevice(d.id));
-  if (slots > d.slot_cap) {
-    uint32_t n = std::max<uint32_t>(slots, d.slot_cap * 2);
-    if (d.slot_mem) (void)hipFree(d.slot_mem);
-    if (d.d_slots) (void)hipFree(d.d_slots);
-    d.slot_mem = nullptr;
-    d.d_slots = nullptr;
-    HIPCHK(hipMalloc(&d.slot_mem, bgv_slot_bytes() * n));
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&d.d_slots), sizeof(bgv_dslot) * n));
-    d.slot_cap = n;
+static int exec_reserve(Exec& x, uint32_t slots, uint32_t groups, size_t nidx, size_t npkb) {
+  if (slots > x.slot_cap) {
+    uint32_t n = std::max<uint32_t>(slots, x.slot_cap * 2);
+    if (x.slot_mem) (void)hipFree(x.slot_mem);
+    if (x.d_slots) (void)hipFree(x.d_slots);
+    x.slot_mem = nullptr;
+    x.d_slots = nullptr;
+    HIPCHK(hipMalloc(&x.slot_mem, bgv_slot_bytes() * n));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_slots), sizeof(bgv_dslot) * n));
+    x.slot_cap = n;
   }
-  if (groups > d.group_cap) {
-    uint32_t n = std::max<uint32_t>(groups, d.group_cap * 2);
-    if (d.group_mem) (void)hipFree(d.group_mem);
-    if (d.d_groups) (void)hipFree(d.d_groups);
-    d.group_mem = nullptr;
-    d.d_groups = nullptr;
-    HIPCHK(hipMalloc(&d.group_mem, bgv_group_bytes() * n));
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&d.d_groups), sizeof(bgv_dgroup) * n));
-    d.group_cap = n;
+  if (groups > x.group_cap) {
+    uint32_t n = std::max<uint32_t>(groups, x.group_cap * 2);
+    if (x.group_mem) (void)hipFree(x.group_mem);
+    if (x.d_groups) (void)hipFree(x.d_groups);
+    x.group_mem = nullptr;
+    x.d_groups = nullptr;
+    HIPCHK(hipMalloc(&x.group_mem, bgv_group_bytes() * n));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_groups), sizeof(bgv_dgroup) * n));
+    x.group_cap = n;
   }
   int rc;
-  if ((rc = grow(&d.d_idx, &d.idx_cap, std::max<size_t>(nidx, 1)))) return rc;
-  if ((rc = grow(&d.d_pkb, &d.pkb_cap, std::max<size_t>(npkb, 1)))) return rc;
+  if ((rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1)))) return rc;
+  if ((rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1)))) return rc;
   return BGV_OK;
+}
+
+static int exec_create(Exec* x) {
+  HIPCHK(hipStreamCreateWithFlags(&x->main, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&x->aux[0], hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&x->aux[1], hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&x->fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&x->join[0], hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&x->join[1], hipEventDisableTiming));
+  HIPCHK(hipEventCreate(&x->ev0));
+  HIPCHK(hipEventCreate(&x->ev1));
+  for (auto& e : x->kev) HIPCHK(hipEventCreate(&e));
+  return BGV_OK;
+}
+
+static void exec_destroy(Exec* x) {
+  (void)hipStreamSynchronize(x->main);
+  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  hipEvent_t evs[] = {x->fork, x->join[0], x->join[1], x->ev0, x->ev1};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : x->kev)
+    if (e) (void)hipEventDestroy(e);
+  hipStream_t sts[] = {x->main, x->aux[0], x->aux[1]};
+  for (hipStream_t s : sts)
+    if (s) (void)hipStreamDestroy(s);
+  delete x;
+}
+
+// Take a free exec, preferring device `pref`; blocks while all are busy.
+static std::pair<Device*, Exec*> exec_acquire(bgv_ctx* c, size_t pref) {
+  std::unique_lock<std::mutex> lk(c->exec_mu);
+  for (;;) {
+    for (size_t k = 0; k < c->devs.size(); ++k) {
+      Device& d = c->devs[(pref + k) % c->devs.size()];
+      if (!d.free_execs.empty()) {
+        Exec* x = d.free_execs.back();
+        d.free_execs.pop_back();
+        return {&d, x};
+      }
+    }
+    c->exec_cv.wait(lk);
+  }
+}
+
+static void exec_release(bgv_ctx* c, Device* d, Exec* x) {
+  {
+    std::lock_guard<std::mutex> lk(c->exec_mu);
+    d->free_execs.push_back(x);
+  }
+  c->exec_cv.notify_one();
 }
 
 // ---------------------------------------------------------------------------
@@ -166,16 +232,17 @@ namespace {
 struct Layout {
   std::vector<bgv_dslot> slots;
   std::vector<bgv_dgroup> groups;
-  std::vector<int32_t> slot_set;       // set index per slot (-1 = pad)
+  std::vector<int32_t> slot_set;  // set index per slot (-1 = pad)
   std::vector<std::vector<uint32_t>> job_groups;
-  std::vector<char> group_shared;      // group holds sets of more than one job
-  std::vector<uint32_t> idx;           // concatenated pubkey indices
-  std::vector<uint8_t> pkb;            // concatenated 96-B pubkey records
+  std::vector<uint32_t> job_first_slot;  // first slot of each laid-out job (its slots are contiguous)
+  std::vector<char> group_shared;        // group holds sets of more than one job
+  std::vector<uint32_t> idx;             // concatenated pubkey indices
+  std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
 };
 
 struct Builder {
   Layout& L;
-  bool open = false;       // a group is open for appending
+  bool open = false;  // a group is open for appending
   uint32_t open_group = 0;
   int open_job = -1;
   explicit Builder(Layout& l) : L(l) {}
@@ -200,13 +267,14 @@ struct Builder {
     L.slots.push_back(s);
     L.slot_set.push_back(-1);
   }
-  void add(int job, uint32_t set_index, const bgv_set& st) {
+  void add(int job, uint32_t set_index, const bgv_set& st, bool first_of_job) {
     if (!open || L.groups[open_group].n_slots == BGV_WAVE) new_group();
     bgv_dgroup& g = L.groups[open_group];
     if (open_job >= 0 && open_job != job) L.group_shared[open_group] = 1;
     open_job = job;
     std::vector<uint32_t>& jg = L.job_groups[job];
     if (jg.empty() || jg.back() != open_group) jg.push_back(open_group);
+    if (first_of_job) L.job_first_slot[job] = (uint32_t)L.slots.size();
     bgv_dslot s;
     memset(&s, 0, sizeof(s));
     s.n_pk = st.n_pk;
@@ -230,56 +298,30 @@ struct Builder {
 };
 }  // namespace
 
-// Run one layout on the context's first device; fills per-slot statuses and per-group verdicts.
-static int run_layout(bgv_ctx* c, Layout& L, std::vector<int32_t>& sig_st, std::vector<int32_t>& pk_st,
-                      std::vector<int32_t>& verdict, double* dev_ms) {
-  const uint32_t nslots = (uint32_t)L.slots.size(), ngroups = (uint32_t)L.groups.size();
-  sig_st.assign(nslots, 0);
-  pk_st.assign(nslots, 0);
-  verdict.assign(ngroups, 0);
-  if (nslots == 0) return BGV_OK;
-  std::vector<uint64_t> sc(nslots);
-  fill_scalars(c, sc.data(), nslots);
-  for (uint32_t i = 0; i < nslots; ++i) L.slots[i].scalar = sc[i];
+static void prof_add(bgv_ctx* c, Exec& x, bool sets, bool groups) {
+  std::lock_guard<std::mutex> lk(c->prof_mu);
+  if (!c->profile) return;
+  for (int k = 0; k < BGV_NKERNELS; ++k) {
+    const bool is_set_kernel = k < 4;
+    if ((is_set_kernel && !sets) || (!is_set_kernel && !groups)) continue;
+    float km = 0;
+    if (hipEventElapsedTime(&km, x.kev[2 * k], x.kev[2 * k + 1]) == hipSuccess) c->kernel_ms[k] += km;
+  }
+  if (sets) c->kernel_launches++;
+}
 
-  Device& d = c->devs[0];
-  int rc = ensure_device_capacity(d, nslots, ngroups, L.idx.size(), L.pkb.size());
-  if (rc) return rc;
-  HIPCHK(hipSetDevice(d.id));
-  HIPCHK(hipMemcpyAsync(d.d_slots, L.slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, d.stream));
-  HIPCHK(hipMemcpyAsync(d.d_groups, L.groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, d.stream));
-  if (!L.idx.empty())
-    HIPCHK(hipMemcpyAsync(d.d_idx, L.idx.data(), 4 * L.idx.size(), hipMemcpyHostToDevice, d.stream));
-  if (!L.pkb.empty()) HIPCHK(hipMemcpyAsync(d.d_pkb, L.pkb.data(), L.pkb.size(), hipMemcpyHostToDevice, d.stream));
+static bgv_dev_batch make_batch(Device& d, Exec& x, uint32_t nslots, uint32_t ngroups) {
   bgv_dev_batch b;
   memset(&b, 0, sizeof(b));
   b.nslots = nslots;
   b.ngroups = ngroups;
-  b.slots = d.d_slots;
-  b.groups = d.d_groups;
-  b.pk_idx = d.d_idx;
+  b.slots = x.d_slots;
+  b.groups = x.d_groups;
+  b.pk_idx = x.d_idx;
   b.cache_opaque = d.cache;
-  b.pk_bytes = d.d_pkb;
-  bgv_carve(&b, d.slot_mem, d.slot_cap, d.group_mem, d.group_cap);
-  HIPCHK(hipEventRecord(d.ev0, d.stream));
-  HIPCHK(bgv_launch_verify(b, d.stream, c->profile ? d.kev : nullptr));
-  HIPCHK(hipEventRecord(d.ev1, d.stream));
-  HIPCHK(hipMemcpyAsync(sig_st.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(hipMemcpyAsync(pk_st.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(hipMemcpyAsync(verdict.data(), b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(hipStreamSynchronize(d.stream));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
-  if (dev_ms) *dev_ms += ms;
-  if (c->profile) {
-    for (int k = 0; k < BGV_NKERNELS; ++k) {
-      float km = 0;
-      HIPCHK(hipEventElapsedTime(&km, d.kev[k], d.kev[k + 1]));
-      c->kernel_ms[k] += km;
-    }
-    c->kernel_launches++;
-  }
-  return BGV_OK;
+  b.pk_bytes = x.d_pkb;
+  bgv_carve(&b, x.slot_mem, x.slot_cap, x.group_mem, x.group_cap);
+  return b;
 }
 
 // Outcome of one job from its slots' statuses (maybeBatch.ts:16-39 + blst semantics):
@@ -309,6 +351,7 @@ static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_
   if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
   if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
 
+  std::shared_lock<std::shared_mutex> cache_lock(c->cache_mu);
   // host-side argument checks that the reference raises before any crypto
   std::vector<int32_t> code(njobs, 2);
   for (size_t j = 0; j < njobs; ++j) {
@@ -320,8 +363,10 @@ static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_
     }
     for (uint32_t k = 0; k < jb.n_sets && code[j] == 2; ++k) {
       const bgv_set& s = sets[jb.first_set + k];
-      if (s.n_pk == 0) code[j] = -BGV_E_EMPTY_AGGREGATE;
-      else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes)) return -BGV_E_ARG;
+      if (s.n_pk == 0)
+        code[j] = -BGV_E_EMPTY_AGGREGATE;
+      else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes))
+        return -BGV_E_ARG;
       else if (s.pk_indices)
         for (uint32_t q = 0; q < s.n_pk; ++q)
           if (s.pk_indices[q] >= c->n_pubkeys) {
@@ -331,49 +376,83 @@ static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_
     }
   }
 
-  std::lock_guard<std::mutex> lk(c->mu);
-  std::vector<int32_t> set_sig(nsets, 0), set_pk(nsets, 0);
-  std::vector<size_t> retry;
-  for (int pass = 0; pass < 2; ++pass) {
-    Layout L;
-    L.job_groups.resize(njobs);
-    Builder B(L);
-    std::vector<size_t> todo;
-    if (pass == 0) {
-      for (size_t j = 0; j < njobs; ++j)
-        if (code[j] == 2) todo.push_back(j);
-    } else {
-      todo = retry;
-    }
-    if (todo.empty()) break;
-    // batchable jobs share groups (pass 0, worker mode); everything else is exclusive
-    for (size_t j : todo) {
-      const bool shared = pass == 0 && mode == BGV_MODE_WORKER && jobs[j].batchable;
-      if (shared) continue;
-      B.close_group();
-      for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
-        B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k]);
-      B.close_group();
-    }
+  // ---- pass 1: lay out every job; batchable jobs (worker mode) share groups ----
+  Layout L;
+  L.job_groups.resize(njobs);
+  L.job_first_slot.assign(njobs, 0);
+  Builder B(L);
+  std::vector<size_t> todo;
+  for (size_t j = 0; j < njobs; ++j)
+    if (code[j] == 2) todo.push_back(j);
+  auto shared_job = [&](size_t j) { return mode == BGV_MODE_WORKER && jobs[j].batchable; };
+  for (size_t j : todo) {
+    if (shared_job(j)) continue;
     B.close_group();
-    for (size_t j : todo) {
-      const bool shared = pass == 0 && mode == BGV_MODE_WORKER && jobs[j].batchable;
-      if (!shared) continue;
-      for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
-        B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k]);
+    for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
+      B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
+    B.close_group();
+  }
+  B.close_group();
+  for (size_t j : todo) {
+    if (!shared_job(j)) continue;
+    for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
+      B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
+  }
+  const uint32_t nslots = (uint32_t)L.slots.size(), ngroups = (uint32_t)L.groups.size();
+  std::vector<int32_t> ss(nslots, 0), ps(nslots, 0), verdict(ngroups, 0);
+  std::vector<int32_t> set_sig(nsets, 0), set_pk(nsets, 0);
+
+  if (nslots) {
+    std::vector<uint64_t> sc(nslots);
+    fill_scalars(c, sc.data(), nslots);
+    for (uint32_t i = 0; i < nslots; ++i) L.slots[i].scalar = sc[i];
+    auto dx = exec_acquire(c, c->rr++);
+    Device& d = *dx.first;
+    Exec& x = *dx.second;
+    struct Release {
+      bgv_ctx* c;
+      Device* d;
+      Exec* x;
+      ~Release() { exec_release(c, d, x); }
+    } rel{c, &d, &x};
+    bool prof;
+    {
+      std::lock_guard<std::mutex> lk(c->prof_mu);
+      prof = c->profile;
     }
-    std::vector<int32_t> ss, ps, verdict;
-    int rc = run_layout(c, L, ss, ps, verdict, &st.device_ms);
+    HIPCHK(hipSetDevice(d.id));
+    int rc = exec_reserve(x, nslots, std::max<uint32_t>(ngroups, (uint32_t)njobs), L.idx.size(), L.pkb.size());
     if (rc) return rc;
-    st.device_groups += L.groups.size();
-    for (size_t i = 0; i < L.slots.size(); ++i)
+    HIPCHK(hipMemcpyAsync(x.d_slots, L.slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
+    HIPCHK(hipMemcpyAsync(x.d_groups, L.groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
+    if (!L.idx.empty())
+      HIPCHK(hipMemcpyAsync(x.d_idx, L.idx.data(), 4 * L.idx.size(), hipMemcpyHostToDevice, x.main));
+    if (!L.pkb.empty()) HIPCHK(hipMemcpyAsync(x.d_pkb, L.pkb.data(), L.pkb.size(), hipMemcpyHostToDevice, x.main));
+    bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
+    bgv_streams S{x.main, {x.aux[0], x.aux[1]}, x.fork, {x.join[0], x.join[1]}, prof ? x.kev : nullptr};
+    HIPCHK(hipEventRecord(x.ev0, x.main));
+    HIPCHK(bgv_launch_sets(b, S));
+    HIPCHK(bgv_launch_groups(b, S));
+    HIPCHK(hipEventRecord(x.ev1, x.main));
+    HIPCHK(hipMemcpyAsync(ss.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
+    HIPCHK(hipMemcpyAsync(ps.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
+    HIPCHK(hipMemcpyAsync(verdict.data(), b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.main));
+    HIPCHK(hipStreamSynchronize(x.main));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+    st.device_ms += ms;
+    if (prof) prof_add(c, x, true, true);
+    st.device_groups += ngroups;
+    for (uint32_t i = 0; i < nslots; ++i)
       if (L.slot_set[i] >= 0) {
         set_sig[L.slot_set[i]] = ss[i];
         set_pk[L.slot_set[i]] = ps[i];
         st.sets_verified++;
       }
-    retry.clear();
-    std::vector<char> group_retried(L.groups.size(), 0);
+
+    // ---- verdicts; jobs in failing mixed groups are re-verified alone ----
+    std::vector<size_t> retry;
+    std::vector<char> group_retried(ngroups, 0);
     for (size_t j : todo) {
       int32_t pre = job_precheck(set_sig, set_pk, jobs[j]);
       if (pre != 2) {
@@ -393,10 +472,47 @@ static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_
         retry.push_back(j);
       } else {
         code[j] = ok ? 1 : 0;
-        if (ok && pass == 0 && mode == BGV_MODE_WORKER && jobs[j].batchable) st.batch_sigs_success += jobs[j].n_sets;
+        if (ok && shared_job(j)) st.batch_sigs_success += jobs[j].n_sets;
       }
     }
     for (char r : group_retried) st.batch_retries += r;
+
+    // ---- pass 2: per-job groups over the per-slot results already on the device.
+    // Each retried job gets its own final exponentiation: the same equation as
+    // verifying the job alone, with the same nonzero randomizers.
+    if (!retry.empty()) {
+      std::vector<bgv_dgroup> rg;
+      std::vector<std::vector<uint32_t>> jg(retry.size());
+      for (size_t q = 0; q < retry.size(); ++q) {
+        const size_t j = retry[q];
+        for (uint32_t off = 0; off < jobs[j].n_sets; off += BGV_WAVE) {
+          jg[q].push_back((uint32_t)rg.size());
+          rg.push_back(bgv_dgroup{L.job_first_slot[j] + off, std::min<uint32_t>(BGV_WAVE, jobs[j].n_sets - off)});
+        }
+      }
+      const uint32_t nrg = (uint32_t)rg.size();
+      if (nrg > x.group_cap) {
+        rc = exec_reserve(x, nslots, nrg, L.idx.size(), L.pkb.size());
+        if (rc) return rc;
+      }
+      std::vector<int32_t> rv(nrg, 0);
+      HIPCHK(hipMemcpyAsync(x.d_groups, rg.data(), sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.main));
+      b = make_batch(d, x, nslots, nrg);
+      HIPCHK(hipEventRecord(x.ev0, x.main));
+      HIPCHK(bgv_launch_groups(b, S));
+      HIPCHK(hipEventRecord(x.ev1, x.main));
+      HIPCHK(hipMemcpyAsync(rv.data(), b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.main));
+      HIPCHK(hipStreamSynchronize(x.main));
+      HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+      st.device_ms += ms;
+      if (prof) prof_add(c, x, false, true);
+      st.device_groups += nrg;
+      for (size_t q = 0; q < retry.size(); ++q) {
+        bool ok = true;
+        for (uint32_t g : jg[q]) ok = ok && rv[g];
+        code[retry[q]] = ok ? 1 : 0;
+      }
+    }
   }
   for (size_t j = 0; j < njobs; ++j) out[j] = code[j] == 2 ? -BGV_E_DEVICE : code[j];
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -430,6 +546,20 @@ static void worker_loop(bgv_ctx* c) {
   }
 }
 
+static void ctx_free_devices(bgv_ctx* c) {
+  for (Device& d : c->devs) {
+    (void)hipSetDevice(d.id);
+    for (Exec* x : d.all_execs) exec_destroy(x);
+    d.all_execs.clear();
+    d.free_execs.clear();
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    if (d.cache) (void)hipFree(d.cache);
+    d.cache = nullptr;
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    d.stream = nullptr;
+  }
+}
+
 int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   if (!out) return -BGV_E_ARG;
   *out = nullptr;
@@ -437,27 +567,25 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   if (avail <= 0) return -BGV_E_DEVICE;
   bgv_ctx* c = new bgv_ctx();
   const int n = (devices && ndev > 0) ? ndev : 1;
+  c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
-    Device d;
+    Device& d = c->devs[i];
     d.id = (devices && ndev > 0) ? devices[i] : 0;
-    if (d.id < 0 || d.id >= avail) {
-      delete c;
-      return -BGV_E_ARG;
+    bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
+              hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; ok && k < BGV_EXECS_PER_DEVICE; ++k) {
+      Exec* x = new Exec();
+      d.all_execs.push_back(x);
+      d.free_execs.push_back(x);
+      ok = exec_create(x) == BGV_OK;
     }
-    if (hipSetDevice(d.id) != hipSuccess || hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&d.ev0) != hipSuccess || hipEventCreate(&d.ev1) != hipSuccess) {
-      delete c;
-      return -BGV_E_DEVICE;
-    }
-    bool ok = true;
-    for (auto& e : d.kev) ok = ok && hipEventCreate(&e) == hipSuccess;
     if (!ok) {
+      ctx_free_devices(c);
       delete c;
-      return -BGV_E_DEVICE;
+      return d.id < 0 || d.id >= avail ? -BGV_E_ARG : -BGV_E_DEVICE;
     }
-    c->devs.push_back(d);
   }
-  c->worker = std::thread(worker_loop, c);
+  for (int k = 0; k < n * BGV_EXECS_PER_DEVICE; ++k) c->workers.emplace_back(worker_loop, c);
   *out = c;
   return BGV_OK;
 }
@@ -469,21 +597,12 @@ int bgv_close(bgv_ctx* c) {
     c->stop = true;
   }
   c->qcv.notify_all();
-  if (c->worker.joinable()) c->worker.join();
-  std::lock_guard<std::mutex> lk(c->mu);
-  if (c->closed) return BGV_OK;
-  c->closed = true;
-  for (Device& d : c->devs) {
-    (void)hipSetDevice(d.id);
-    (void)hipStreamSynchronize(d.stream);
-    void* ptrs[] = {d.cache, d.slot_mem, d.group_mem, d.d_slots, d.d_groups, d.d_idx, d.d_pkb, d.d_tmp};
-    for (void* p : ptrs)
-      if (p) (void)hipFree(p);
-    for (auto& e : d.kev) (void)hipEventDestroy(e);
-    (void)hipEventDestroy(d.ev0);
-    (void)hipEventDestroy(d.ev1);
-    (void)hipStreamDestroy(d.stream);
-  }
+  for (auto& w : c->workers)
+    if (w.joinable()) w.join();
+  c->workers.clear();
+  std::unique_lock<std::shared_mutex> lk(c->cache_mu);
+  if (c->closed.exchange(true)) return BGV_OK;
+  ctx_free_devices(c);
   return BGV_OK;
 }
 
@@ -496,7 +615,7 @@ int bgv_destroy(bgv_ctx* c) {
 
 int bgv_set_rng_seed(bgv_ctx* c, uint64_t seed) {
   if (!c) return -BGV_E_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->rng_mu);
   c->rng_seed = seed;
   c->rng_state = seed;
   return BGV_OK;
@@ -504,13 +623,32 @@ int bgv_set_rng_seed(bgv_ctx* c, uint64_t seed) {
 
 size_t bgv_pubkeys_count(const bgv_ctx* c) { return c ? c->n_pubkeys : 0; }
 
-static int cache_reserve(bgv_ctx* c, size_t need);
+// grow every device's cache to hold `need` entries (contents preserved); caller holds cache_mu exclusively
+static int cache_reserve(bgv_ctx* c, size_t need) {
+  const size_t esz = bgv_cache_entry_bytes();
+  for (Device& d : c->devs) {
+    HIPCHK(hipSetDevice(d.id));
+    if (need <= d.cache_cap) continue;
+    size_t cap = std::max(need, d.cache_cap * 2);
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, esz * cap));
+    if (d.cache) {
+      HIPCHK(hipMemcpyAsync(p, d.cache, esz * c->n_pubkeys, hipMemcpyDeviceToDevice, d.stream));
+      HIPCHK(hipStreamSynchronize(d.stream));
+      HIPCHK(hipFree(d.cache));
+    }
+    d.cache = static_cast<bgv_cache_entry*>(p);
+    d.cache_cap = cap;
+  }
+  return BGV_OK;
+}
 
 int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, int fmt) {
   if (!c || (n && !keys) || (fmt != BGV_PK_COMPRESSED && fmt != BGV_PK_UNCOMPRESSED)) return -BGV_E_ARG;
   if (c->closed) return -BGV_E_CLOSED;
+  std::unique_lock<std::shared_mutex> lk(c->cache_mu);
   if ((size_t)first > c->n_pubkeys) return -BGV_E_ARG;  // append or overwrite, no holes
-  std::lock_guard<std::mutex> lk(c->mu);
+  if (n == 0) return BGV_OK;
   const size_t need = (size_t)first + n;
   const size_t esz = bgv_cache_entry_bytes();
   int first_err = BGV_OK;
@@ -569,9 +707,10 @@ int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out
   if (!c || !out96 || (n && !idx)) return -BGV_E_ARG;
   if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return -BGV_E_EMPTY_AGGREGATE;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);
   for (size_t i = 0; i < n; ++i)
     if (idx[i] >= c->n_pubkeys) return -BGV_E_BAD_INDEX;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];
   HIPCHK(hipSetDevice(d.id));
   uint32_t* di = nullptr;
@@ -599,7 +738,7 @@ int bgv_hash_to_g2(bgv_ctx* c, const uint8_t* msgs, const uint32_t* lens, size_t
     tot += lens[i];
   }
   if (tot && !msgs) return -BGV_E_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];
   HIPCHK(hipSetDevice(d.id));
   uint8_t *dm = nullptr, *dout = nullptr;
@@ -621,32 +760,12 @@ int bgv_hash_to_g2(bgv_ctx* c, const uint8_t* msgs, const uint32_t* lens, size_t
   return BGV_OK;
 }
 
-// grow every device's cache to hold `need` entries (contents preserved)
-static int cache_reserve(bgv_ctx* c, size_t need) {
-  const size_t esz = bgv_cache_entry_bytes();
-  for (Device& d : c->devs) {
-    HIPCHK(hipSetDevice(d.id));
-    if (need <= d.cache_cap) continue;
-    size_t cap = std::max(need, d.cache_cap * 2);
-    void* p = nullptr;
-    HIPCHK(hipMalloc(&p, esz * cap));
-    if (d.cache) {
-      HIPCHK(hipMemcpyAsync(p, d.cache, esz * c->n_pubkeys, hipMemcpyDeviceToDevice, d.stream));
-      HIPCHK(hipStreamSynchronize(d.stream));
-      HIPCHK(hipFree(d.cache));
-    }
-    d.cache = static_cast<bgv_cache_entry*>(p);
-    d.cache_cap = cap;
-  }
-  return BGV_OK;
-}
-
 int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48) {
   if (!c || (n && !sks)) return -BGV_E_ARG;
   if (c->closed) return -BGV_E_CLOSED;
+  std::unique_lock<std::shared_mutex> clk(c->cache_mu);
   if (cache_first > (int64_t)c->n_pubkeys) return -BGV_E_ARG;
   if (n == 0) return BGV_OK;
-  std::lock_guard<std::mutex> lk(c->mu);
   if (cache_first >= 0) {
     int rc = cache_reserve(c, (size_t)cache_first + n);
     if (rc) return rc;
@@ -677,7 +796,7 @@ int bgv_sign(bgv_ctx* c, const uint8_t* sks, const uint8_t* msgs, size_t n, uint
   if (!c || (n && (!sks || !msgs || !out96))) return -BGV_E_ARG;
   if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return BGV_OK;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];
   HIPCHK(hipSetDevice(d.id));
   uint8_t *dsk = nullptr, *dm = nullptr, *dout = nullptr;
@@ -697,7 +816,7 @@ int bgv_sign(bgv_ctx* c, const uint8_t* sks, const uint8_t* msgs, size_t n, uint
 
 int bgv_profile(bgv_ctx* c, int enable, double* kernel_ms, const char** names, int n, uint64_t* launches) {
   if (!c) return -BGV_E_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->prof_mu);
   for (int k = 0; k < n && k < BGV_NKERNELS; ++k) {
     if (kernel_ms) kernel_ms[k] = c->kernel_ms[k];
     if (names) names[k] = BGV_KERNEL_NAMES[k];

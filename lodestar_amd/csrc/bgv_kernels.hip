@@ -277,29 +277,52 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 
-hipError_t bgv_launch_verify(const bgv_dev_batch& b, hipStream_t st, hipEvent_t* ev) {
+// Per-set kernels.  k_sig, k_hash and k_pk are independent and run concurrently
+// on three streams (3x the wavefronts in flight of one set per lane); k_miller
+// joins them on the main stream.
+hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
-  // ev (optional): BGV_NKERNELS + 1 events bracketing each kernel, for per-kernel timing
-#define BGV_MARK(i) \
+  hipEvent_t* ev = s.kev;  // optional: [2k] start / [2k+1] end of kernel k
+#define BGV_MARK(i, st) \
   if (ev) (void)hipEventRecord(ev[i], st)
-  BGV_MARK(0);
-  hipLaunchKernelGGL(k_sig, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.rsig, b.sig_status);
-  BGV_MARK(1);
-  hipLaunchKernelGGL(k_hash, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.h);
-  BGV_MARK(2);
-  hipLaunchKernelGGL(k_pk, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.pk_idx,
+  (void)hipEventRecord(s.fork, s.main);
+  (void)hipStreamWaitEvent(s.aux[0], s.fork, 0);
+  (void)hipStreamWaitEvent(s.aux[1], s.fork, 0);
+  BGV_MARK(0, s.aux[0]);
+  hipLaunchKernelGGL(k_sig, dim3(nblk(n, 64)), dim3(64), 0, s.aux[0], b.slots, n, b.rsig, b.sig_status);
+  BGV_MARK(1, s.aux[0]);
+  BGV_MARK(2, s.main);
+  hipLaunchKernelGGL(k_hash, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.h);
+  BGV_MARK(3, s.main);
+  BGV_MARK(4, s.aux[1]);
+  hipLaunchKernelGGL(k_pk, dim3(nblk(n, 64)), dim3(64), 0, s.aux[1], b.slots, n, b.pk_idx,
                      reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status);
-  BGV_MARK(3);
-  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, st, b.slots, n, b.rpk, b.h, b.sig_status, b.pk_status,
-                     b.f);
-  BGV_MARK(4);
+  BGV_MARK(5, s.aux[1]);
+  (void)hipEventRecord(s.join[0], s.aux[0]);
+  (void)hipEventRecord(s.join[1], s.aux[1]);
+  (void)hipStreamWaitEvent(s.main, s.join[0], 0);
+  (void)hipStreamWaitEvent(s.main, s.join[1], 0);
+  BGV_MARK(6, s.main);
+  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
+                     b.pk_status, b.f);
+  BGV_MARK(7, s.main);
+  return hipGetLastError();
+}
+
+// Per-group kernels over b.groups (contiguous slot ranges of <= 64 slots): used for
+// the first pass and, over the same per-slot results, for the per-job retry pass.
+hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
+  if (b.ngroups == 0) return hipSuccess;
+  hipEvent_t* ev = s.kev;
   const size_t lds = BGV_WAVE * (sizeof(fp12_t) + sizeof(g2_jac));
-  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, st, b.groups, b.f, b.rsig, b.sig_status, b.pk_status,
-                     b.fg, b.sg);
-  BGV_MARK(5);
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.fg, b.sg, b.verdict);
-  BGV_MARK(6);
+  BGV_MARK(8, s.main);
+  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.rsig, b.sig_status,
+                     b.pk_status, b.fg, b.sg);
+  BGV_MARK(9, s.main);
+  BGV_MARK(10, s.main);
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.sg, b.verdict);
+  BGV_MARK(11, s.main);
 #undef BGV_MARK
   return hipGetLastError();
 }

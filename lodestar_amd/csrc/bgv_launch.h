@@ -43,7 +43,13 @@ struct bgv_dev_batch {
 // kernels of one verify launch, in order (names for per-kernel timing)
 #define BGV_NKERNELS 6
 static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_sig", "k_hash", "k_pk", "k_miller", "k_reduce", "k_final"};
-hipError_t bgv_launch_verify(const bgv_dev_batch& b, hipStream_t st, hipEvent_t* ev);
+struct bgv_streams {
+  hipStream_t main, aux[2];
+  hipEvent_t fork, join[2];
+  hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr
+};
+hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);
+hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s);
 size_t bgv_slot_bytes();
 size_t bgv_group_bytes();
 size_t bgv_cache_entry_bytes();

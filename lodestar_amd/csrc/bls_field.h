@@ -184,8 +184,18 @@ BGV_HD fp_t fp_neg(const fp_t& a) {
 // Montgomery product, row-wise over 28-bit limbs (R = 2^392).  Each of the 14
 // u64 accumulators receives at most 2 products per row (< 2^58 + 2^56) over
 // 14 rows plus carries: < 2^63, so no carry ever leaves an accumulator early.
-BGV_MUL_ATTR fp_t fp_mul(fp_t a, fp_t b) {
+// The out-of-line products take their limbs as 28 / 14 scalar arguments: the
+// AMDGPU calling convention passes those in VGPRs v0..v27, whereas a second
+// struct argument would travel through scratch memory on every call.
+#define BGV_L14(p) p##0, p##1, p##2, p##3, p##4, p##5, p##6, p##7, p##8, p##9, p##10, p##11, p##12, p##13
+#define BGV_U14(p)                                                                                        \
+  uint32_t p##0, uint32_t p##1, uint32_t p##2, uint32_t p##3, uint32_t p##4, uint32_t p##5, uint32_t p##6, \
+      uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11, uint32_t p##12, uint32_t p##13
+#define BGV_V14(x) x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11], x.v[12], x.v[13]
+
+BGV_MUL_ATTR fp_t fp_mul_l(BGV_U14(a_), BGV_U14(b_)) {
   BGV_COUNT_MUL();
+  const fp_t a = {{BGV_L14(a_)}}, b = {{BGV_L14(b_)}};
   const uint32_t P_[NL] = BGV_P_LIMBS;
   uint64_t t[NL];
   BGV_UNROLL for (int j = 0; j < NL; ++j) t[j] = 0;
@@ -208,8 +218,9 @@ BGV_MUL_ATTR fp_t fp_mul(fp_t a, fp_t b) {
 }
 
 // Montgomery square: 105 products (cross terms doubled) then 14 reduction rows.
-BGV_MUL_ATTR fp_t fp_sqr(fp_t a) {
+BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
   BGV_COUNT_SQR();
+  const fp_t a = {{BGV_L14(a_)}};
   const uint32_t P_[NL] = BGV_P_LIMBS;
   uint64_t t[2 * NL];
   BGV_UNROLL for (int j = 0; j < 2 * NL; ++j) t[j] = 0;
@@ -231,6 +242,9 @@ BGV_MUL_ATTR fp_t fp_sqr(fp_t a) {
   r.v[NL - 1] = (uint32_t)t[2 * NL - 1];
   return r;
 }
+
+BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_mul_l(BGV_V14(a), BGV_V14(b)); }
+BGV_HD fp_t fp_sqr(const fp_t& a) { return fp_sqr_l(BGV_V14(a)); }
 
 // canonical representative in [0, p) of a weakly reduced value
 BGV_HD fp_t fp_canon(const fp_t& a) {
@@ -380,14 +394,14 @@ BGV_HD fp2_t fp2_dbl(const fp2_t& a) { return fp2_t{fp_dbl(a.c0), fp_dbl(a.c1)};
 BGV_HD fp2_t fp2_neg(const fp2_t& a) { return fp2_t{fp_neg(a.c0), fp_neg(a.c1)}; }
 BGV_HD fp2_t fp2_conj(const fp2_t& a) { return fp2_t{a.c0, fp_neg(a.c1)}; }
 
-BGV_NOINLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   fp_t t0 = fp_mul(a.c0, b.c0);
   fp_t t1 = fp_mul(a.c1, b.c1);
   fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return fp2_t{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
-BGV_NOINLINE fp2_t fp2_sqr(const fp2_t& a) {
+BGV_HD fp2_t fp2_sqr(const fp2_t& a) {
   fp_t t = fp_mul(a.c0, a.c1);
   return fp2_t{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
 }

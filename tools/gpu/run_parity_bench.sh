@@ -1,9 +1,18 @@
+#!/bin/bash
+# GPU-box script: parity tests, smoke, bench, rocprof kernel-trace summary.
 set -o pipefail
-export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 3 --warmup 1 > gpurun_out/bench.json 2> gpurun_out/bench.err
-echo "bench rc=$?"
-tail -5 gpurun_out/pytest_gpu.log; cat gpurun_out/smoke.log gpurun_out/bench.json; tail -5 gpurun_out/bench.err
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+timeout -k 10 300 python -u -m pytest tests/ -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+for inf in ${INFLIGHT:-1 4 8}; do
+  timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 1 --inflight $inf --no-cpu-baseline > gpurun_out/bench_inf$inf.json 2> gpurun_out/bench_inf$inf.err || exit $?
+  cat gpurun_out/bench_inf$inf.json
+done
+if [ -n "$PROF" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --inflight 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || exit $?
+  find gpurun_out/prof_$TAG -name "*stats*" | head
+fi
