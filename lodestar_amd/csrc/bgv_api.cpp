@@ -1,15 +1,23 @@
 // libblsgpu: C-ABI host orchestration of the MI355X batch BLS verifier.
 //
-// Mirrors the reference's scheduling semantics, file by file:
+// Mirrors the reference's scheduling semantics:
 //   * per-job verdicts and retry   packages/beacon-node/src/chain/bls/multithread/worker.ts:32-108
 //   * batch vs single verify       packages/beacon-node/src/chain/bls/maybeBatch.ts:16-39
 //   * pubkey aggregation errors    packages/beacon-node/src/chain/bls/utils.ts:5-16
+//   * packing jobs into packages   packages/beacon-node/src/chain/bls/multithread/index.ts:290-401
 // but lays the sets out for the GPU: one lane per set, device groups of <= 64
-// sets (one wavefront) each closed by its own final exponentiation.  A job's
-// verdict is the AND of the groups holding its sets; a group that mixes
-// batchable jobs and fails sends exactly those jobs to a second pass where each
-// is verified alone (the reference retries the whole >=16-job chunk; the
-// per-job verdicts are the same).
+// sets (one wavefront) each closed by its own final exponentiation.
+//
+// Dynamic batching: every bgv_verify / bgv_verify_async call is laid out on the
+// calling thread and queued; dispatcher threads (a few per device, one HIP
+// stream each) merge all queued calls into one device super-batch, run the
+// kernels once over it and hand each call its own verdicts.  This is the GPU
+// form of the reference's prepareWork(), which packs queued jobs into one worker
+// package: concurrent calls share wavefronts instead of competing for queues.
+//
+// A job's verdict is the AND of the groups holding its sets.  A failing group
+// that mixes batchable jobs sends exactly those jobs to retry rounds run over the
+// per-set results already on the device (no set is recomputed).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,25 +25,75 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
-#include <functional>
 #include <mutex>
 #include <shared_mutex>
-#include <atomic>
 #include <thread>
 #include <vector>
 
 #include "../../include/blsgpu.h"
 #include "bgv_launch.h"
 
+// parts a failing mixed group is split into per retry round (BGV_RETRY_FANOUT env)
+#define BGV_RETRY_FANOUT 64
+// slots merged into one device super-batch (BGV_MAX_BATCH_SLOTS env)
+#define BGV_MAX_BATCH_SLOTS 131072
+// dispatcher threads (= HIP streams) per device (BGV_DISPATCHERS env)
+#define BGV_DISPATCHERS 2
+
+static size_t env_size(const char* name, size_t dflt, size_t lo) {
+  const char* e = getenv(name);
+  long n = e ? atol(e) : 0;
+  return n >= (long)lo ? (size_t)n : dflt;
+}
+static size_t retry_fanout() {
+  static const size_t v = env_size("BGV_RETRY_FANOUT", BGV_RETRY_FANOUT, 2);
+  return v;
+}
+static size_t max_batch_slots() {
+  static const size_t v = env_size("BGV_MAX_BATCH_SLOTS", BGV_MAX_BATCH_SLOTS, BGV_WAVE);
+  return v;
+}
+// sets per first-pass device group, a power of two <= 64 (BGV_GROUP_SLOTS env).
+// Smaller groups fail less often under invalid signatures (fewer retried jobs)
+// at the price of more final exponentiations when every set is valid.
+#define BGV_GROUP_SLOTS 64
+static uint32_t group_slots() {
+  static const uint32_t v = [] {
+    size_t n = env_size("BGV_GROUP_SLOTS", BGV_GROUP_SLOTS, 1);
+    uint32_t p = 1;
+    while (p * 2 <= n && p * 2 <= BGV_WAVE) p *= 2;
+    return p;
+  }();
+  return v;
+}
+// how long an idle dispatcher waits for more calls to merge (BGV_COALESCE_US env)
+#define BGV_COALESCE_US 2000
+static size_t coalesce_us() {
+  static const size_t v = env_size("BGV_COALESCE_US", BGV_COALESCE_US, 0);
+  return v;
+}
+static int dispatchers_per_device() {
+  static const int v = (int)env_size("BGV_DISPATCHERS", BGV_DISPATCHERS, 1);
+  return v;
+}
+
+extern "C" int bgv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
 namespace {
 
-// One in-flight verify call on one device: its own streams, events and buffers.
+// One dispatcher's device resources: its stream, events and buffers.
 struct Exec {
-  hipStream_t main = nullptr, aux[2] = {nullptr, nullptr};
-  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr}, ev0 = nullptr, ev1 = nullptr;
+  hipStream_t main = nullptr;   // per-set kernels (compute-bound)
+  hipStream_t close = nullptr;  // group closing + retry rounds (latency-bound): high priority
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_sets = nullptr;
   hipEvent_t kev[2 * BGV_NKERNELS] = {};
   void* slot_mem = nullptr;
   uint32_t slot_cap = 0;
@@ -51,29 +109,122 @@ struct Exec {
 
 struct Device {
   int id = 0;
-  hipStream_t stream = nullptr;  // utility work (cache upload, hooks, keygen)
+  hipStream_t stream = nullptr;      // utility work (cache upload, hooks, keygen)
   bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
   size_t cache_cap = 0;
-  std::vector<Exec*> free_execs;
-  std::vector<Exec*> all_execs;
+  std::vector<Exec*> execs;
+  // held while one super-batch runs its per-set kernels (pointer: Device stays movable)
+  std::unique_ptr<std::mutex> compute_mu = std::make_unique<std::mutex>();
 };
 
-struct Job {  // one async request
-  const bgv_job* jobs;
-  size_t njobs;
-  const bgv_set* sets;
-  size_t nsets;
-  int mode;
-  int32_t* out;
-  bgv_stats* stats;
-  bgv_done_fn done;
-  void* user;
+// jobs -> slots/groups of one call
+struct Layout {
+  std::vector<bgv_dslot> slots;
+  std::vector<bgv_dgroup> groups;
+  std::vector<int32_t> slot_set;  // set index per slot (-1 = pad)
+  std::vector<std::vector<uint32_t>> job_groups;
+  std::vector<uint32_t> job_first_slot;  // first slot of each laid-out job (its slots are contiguous)
+  std::vector<char> group_shared;        // group holds sets of more than one job
+  std::vector<uint32_t> idx;             // concatenated pubkey indices
+  std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
+};
+
+struct Builder {
+  Layout& L;
+  bool open = false;  // a group is open for appending
+  uint32_t open_group = 0;
+  int open_job = -1;
+  explicit Builder(Layout& l) : L(l) {}
+
+  void close_group() { open = false; }
+  void new_group() {
+    // start at the next wave boundary
+    uint32_t first = (uint32_t)L.slots.size();
+    const uint32_t gs = group_slots();
+    uint32_t aligned = (first + gs - 1) / gs * gs;
+    while (L.slots.size() < aligned) pad();
+    L.groups.push_back(bgv_dgroup{aligned, 0});
+    L.group_shared.push_back(0);
+    open_group = (uint32_t)L.groups.size() - 1;
+    open = true;
+    open_job = -1;
+  }
+  void pad() {
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.flags = BGV_SLOT_PAD;
+    L.slots.push_back(s);
+    L.slot_set.push_back(-1);
+  }
+  void pad_to_wave() {
+    while (L.slots.size() % BGV_WAVE) pad();
+  }
+  void add(int job, uint32_t set_index, const bgv_set& st, bool first_of_job) {
+    if (!open || L.groups[open_group].n_slots == group_slots()) new_group();
+    bgv_dgroup& g = L.groups[open_group];
+    if (open_job >= 0 && open_job != job) L.group_shared[open_group] = 1;
+    open_job = job;
+    std::vector<uint32_t>& jg = L.job_groups[job];
+    if (jg.empty() || jg.back() != open_group) jg.push_back(open_group);
+    if (first_of_job) L.job_first_slot[job] = (uint32_t)L.slots.size();
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.n_pk = st.n_pk;
+    s.sig_len = st.sig_len;
+    s.group = open_group;
+    if (st.pk_indices) {
+      s.flags = BGV_SLOT_PK_CACHED;
+      s.pk_off = (uint32_t)L.idx.size();
+      L.idx.insert(L.idx.end(), st.pk_indices, st.pk_indices + st.n_pk);
+    } else {
+      s.flags = BGV_SLOT_PK_BYTES;
+      s.pk_off = (uint32_t)(L.pkb.size() / 96);
+      L.pkb.insert(L.pkb.end(), st.pk_bytes, st.pk_bytes + 96ull * st.n_pk);
+    }
+    memcpy(s.msg, st.msg, 32);
+    if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
+    L.slots.push_back(s);
+    L.slot_set.push_back((int32_t)set_index);
+    g.n_slots++;
+  }
+};
+
+struct Part {  // one retry test: consecutive jobs of one failing unit, and the device groups covering them
+  std::vector<size_t> jobs;
+  std::vector<uint32_t> groups;  // indices into the round's merged group list
+};
+
+// One bgv_verify call travelling through a dispatcher.
+struct Call {
+  const bgv_job* jobs = nullptr;
+  size_t njobs = 0;
+  const bgv_set* sets = nullptr;
+  size_t nsets = 0;
+  int mode = 0;
+  int32_t* out = nullptr;
+  bgv_stats* stats_out = nullptr;
+  bgv_done_fn done = nullptr;
+  void* user = nullptr;
+  bool owned = false;
+  std::chrono::steady_clock::time_point t0;
+  // host state
+  Layout L;
+  std::vector<int32_t> code;  // 2 = pending
+  std::vector<size_t> todo;
+  std::vector<int32_t> set_sig, set_pk;
+  std::vector<std::vector<size_t>> units;  // pending retry units
+  std::vector<Part> parts;
+  bgv_stats st{};
+  uint32_t slot_base = 0;  // offset of this call's slots in the merged batch
+  int rc = BGV_OK;
+  // completion
+  std::mutex mu;
+  std::condition_variable cv;
+  bool finished = false;
+  bool shared_job(size_t j) const { return mode == BGV_MODE_WORKER && jobs[j].batchable; }
 };
 
 }  // namespace
-
-// concurrent verify calls per device (each on its own streams and buffers)
-#define BGV_EXECS_PER_DEVICE 8
 
 struct bgv_ctx {
   std::vector<Device> devs;
@@ -83,18 +234,15 @@ struct bgv_ctx {
   uint64_t rng_seed = 0, rng_state = 0;
   std::shared_mutex cache_mu;  // verify: shared; cache writes: exclusive
   std::mutex util_mu;          // utility streams
-  std::mutex exec_mu;
-  std::condition_variable exec_cv;
-  size_t rr = 0;  // round-robin device for the next call
   std::mutex prof_mu;
   bool profile = false;
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
-  // async workers
-  std::vector<std::thread> workers;
+  // dispatch
+  std::vector<std::thread> dispatchers;
   std::mutex qmu;
   std::condition_variable qcv;
-  std::deque<Job> queue;
+  std::deque<Call*> queue;
   bool stop = false;
 };
 
@@ -145,164 +293,65 @@ static int grow(T** p, size_t* cap, size_t want) {
   return BGV_OK;
 }
 
-static int exec_reserve(Exec& x, uint32_t slots, uint32_t groups, size_t nidx, size_t npkb) {
-  if (slots > x.slot_cap) {
-    uint32_t n = std::max<uint32_t>(slots, x.slot_cap * 2);
-    if (x.slot_mem) (void)hipFree(x.slot_mem);
-    if (x.d_slots) (void)hipFree(x.d_slots);
-    x.slot_mem = nullptr;
-    x.d_slots = nullptr;
-    HIPCHK(hipMalloc(&x.slot_mem, bgv_slot_bytes() * n));
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_slots), sizeof(bgv_dslot) * n));
-    x.slot_cap = n;
-  }
-  if (groups > x.group_cap) {
-    uint32_t n = std::max<uint32_t>(groups, x.group_cap * 2);
-    if (x.group_mem) (void)hipFree(x.group_mem);
-    if (x.d_groups) (void)hipFree(x.d_groups);
-    x.group_mem = nullptr;
-    x.d_groups = nullptr;
-    HIPCHK(hipMalloc(&x.group_mem, bgv_group_bytes() * n));
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_groups), sizeof(bgv_dgroup) * n));
-    x.group_cap = n;
-  }
-  int rc;
-  if ((rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1)))) return rc;
-  if ((rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1)))) return rc;
+static int exec_reserve_slots(Exec& x, uint32_t slots) {
+  if (slots <= x.slot_cap) return BGV_OK;
+  uint32_t n = std::max<uint32_t>(slots, x.slot_cap * 2);
+  if (x.slot_mem) (void)hipFree(x.slot_mem);
+  if (x.d_slots) (void)hipFree(x.d_slots);
+  x.slot_mem = nullptr;
+  x.d_slots = nullptr;
+  HIPCHK(hipMalloc(&x.slot_mem, bgv_slot_bytes() * n));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_slots), sizeof(bgv_dslot) * n));
+  x.slot_cap = n;
+  return BGV_OK;
+}
+
+static int exec_reserve_groups(Exec& x, uint32_t groups) {
+  if (groups <= x.group_cap) return BGV_OK;
+  uint32_t n = std::max<uint32_t>(groups, x.group_cap * 2);
+  if (x.group_mem) (void)hipFree(x.group_mem);
+  if (x.d_groups) (void)hipFree(x.d_groups);
+  x.group_mem = nullptr;
+  x.d_groups = nullptr;
+  HIPCHK(hipMalloc(&x.group_mem, bgv_group_bytes() * n));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_groups), sizeof(bgv_dgroup) * n));
+  x.group_cap = n;
   return BGV_OK;
 }
 
 static int exec_create(Exec* x) {
   HIPCHK(hipStreamCreateWithFlags(&x->main, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&x->aux[0], hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&x->aux[1], hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&x->fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&x->join[0], hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&x->join[1], hipEventDisableTiming));
+  int least = 0, greatest = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  HIPCHK(hipStreamCreateWithPriority(&x->close, hipStreamNonBlocking, greatest));
   HIPCHK(hipEventCreate(&x->ev0));
   HIPCHK(hipEventCreate(&x->ev1));
+  HIPCHK(hipEventCreateWithFlags(&x->ev_sets, hipEventDisableTiming));
   for (auto& e : x->kev) HIPCHK(hipEventCreate(&e));
   return BGV_OK;
 }
 
 static void exec_destroy(Exec* x) {
-  (void)hipStreamSynchronize(x->main);
+  if (x->main) (void)hipStreamSynchronize(x->main);
   void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  hipEvent_t evs[] = {x->fork, x->join[0], x->join[1], x->ev0, x->ev1};
-  for (hipEvent_t e : evs)
-    if (e) (void)hipEventDestroy(e);
+  if (x->ev0) (void)hipEventDestroy(x->ev0);
+  if (x->ev1) (void)hipEventDestroy(x->ev1);
+  if (x->ev_sets) (void)hipEventDestroy(x->ev_sets);
   for (auto& e : x->kev)
     if (e) (void)hipEventDestroy(e);
-  hipStream_t sts[] = {x->main, x->aux[0], x->aux[1]};
-  for (hipStream_t s : sts)
-    if (s) (void)hipStreamDestroy(s);
+  if (x->close) (void)hipStreamSynchronize(x->close);
+  if (x->main) (void)hipStreamDestroy(x->main);
+  if (x->close) (void)hipStreamDestroy(x->close);
   delete x;
 }
-
-// Take a free exec, preferring device `pref`; blocks while all are busy.
-static std::pair<Device*, Exec*> exec_acquire(bgv_ctx* c, size_t pref) {
-  std::unique_lock<std::mutex> lk(c->exec_mu);
-  for (;;) {
-    for (size_t k = 0; k < c->devs.size(); ++k) {
-      Device& d = c->devs[(pref + k) % c->devs.size()];
-      if (!d.free_execs.empty()) {
-        Exec* x = d.free_execs.back();
-        d.free_execs.pop_back();
-        return {&d, x};
-      }
-    }
-    c->exec_cv.wait(lk);
-  }
-}
-
-static void exec_release(bgv_ctx* c, Device* d, Exec* x) {
-  {
-    std::lock_guard<std::mutex> lk(c->exec_mu);
-    d->free_execs.push_back(x);
-  }
-  c->exec_cv.notify_one();
-}
-
-// ---------------------------------------------------------------------------
-// Layout: jobs -> slots/groups
-// ---------------------------------------------------------------------------
-namespace {
-struct Layout {
-  std::vector<bgv_dslot> slots;
-  std::vector<bgv_dgroup> groups;
-  std::vector<int32_t> slot_set;  // set index per slot (-1 = pad)
-  std::vector<std::vector<uint32_t>> job_groups;
-  std::vector<uint32_t> job_first_slot;  // first slot of each laid-out job (its slots are contiguous)
-  std::vector<char> group_shared;        // group holds sets of more than one job
-  std::vector<uint32_t> idx;             // concatenated pubkey indices
-  std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
-};
-
-struct Builder {
-  Layout& L;
-  bool open = false;  // a group is open for appending
-  uint32_t open_group = 0;
-  int open_job = -1;
-  explicit Builder(Layout& l) : L(l) {}
-
-  void close_group() { open = false; }
-  void new_group() {
-    // start at the next wave boundary
-    uint32_t first = (uint32_t)L.slots.size();
-    uint32_t aligned = (first + BGV_WAVE - 1) / BGV_WAVE * BGV_WAVE;
-    while (L.slots.size() < aligned) pad();
-    bgv_dgroup g{aligned, 0};
-    L.groups.push_back(g);
-    L.group_shared.push_back(0);
-    open_group = (uint32_t)L.groups.size() - 1;
-    open = true;
-    open_job = -1;
-  }
-  void pad() {
-    bgv_dslot s;
-    memset(&s, 0, sizeof(s));
-    s.flags = BGV_SLOT_PAD;
-    L.slots.push_back(s);
-    L.slot_set.push_back(-1);
-  }
-  void add(int job, uint32_t set_index, const bgv_set& st, bool first_of_job) {
-    if (!open || L.groups[open_group].n_slots == BGV_WAVE) new_group();
-    bgv_dgroup& g = L.groups[open_group];
-    if (open_job >= 0 && open_job != job) L.group_shared[open_group] = 1;
-    open_job = job;
-    std::vector<uint32_t>& jg = L.job_groups[job];
-    if (jg.empty() || jg.back() != open_group) jg.push_back(open_group);
-    if (first_of_job) L.job_first_slot[job] = (uint32_t)L.slots.size();
-    bgv_dslot s;
-    memset(&s, 0, sizeof(s));
-    s.n_pk = st.n_pk;
-    s.sig_len = st.sig_len;
-    s.group = open_group;
-    if (st.pk_indices) {
-      s.flags = BGV_SLOT_PK_CACHED;
-      s.pk_off = (uint32_t)L.idx.size();
-      L.idx.insert(L.idx.end(), st.pk_indices, st.pk_indices + st.n_pk);
-    } else {
-      s.flags = BGV_SLOT_PK_BYTES;
-      s.pk_off = (uint32_t)(L.pkb.size() / 96);
-      L.pkb.insert(L.pkb.end(), st.pk_bytes, st.pk_bytes + 96ull * st.n_pk);
-    }
-    memcpy(s.msg, st.msg, 32);
-    if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
-    L.slots.push_back(s);
-    L.slot_set.push_back((int32_t)set_index);
-    g.n_slots++;
-  }
-};
-}  // namespace
 
 static void prof_add(bgv_ctx* c, Exec& x, bool sets, bool groups) {
   std::lock_guard<std::mutex> lk(c->prof_mu);
   if (!c->profile) return;
   for (int k = 0; k < BGV_NKERNELS; ++k) {
-    const bool is_set_kernel = k < 4;
+    const bool is_set_kernel = k < BGV_NSETKERNELS;
     if ((is_set_kernel && !sets) || (!is_set_kernel && !groups)) continue;
     float km = 0;
     if (hipEventElapsedTime(&km, x.kev[2 * k], x.kev[2 * k + 1]) == hipSuccess) c->kernel_ms[k] += km;
@@ -342,182 +391,385 @@ static int32_t job_precheck(const std::vector<int32_t>& set_sig, const std::vect
   return 2;
 }
 
-static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
-                       int32_t* out, bgv_stats* stats) {
-  const auto t0 = std::chrono::steady_clock::now();
-  bgv_stats st;
-  memset(&st, 0, sizeof(st));
+// ---------------------------------------------------------------------------
+// Call lifecycle
+// ---------------------------------------------------------------------------
+static void call_finish(Call* call) {
+  for (size_t j = 0; j < call->njobs; ++j) call->out[j] = call->code[j] == 2 ? -BGV_E_DEVICE : call->code[j];
+  call->st.wall_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call->t0).count();
+  if (call->stats_out) *call->stats_out = call->st;
+  if (call->done) call->done(call->user, call->rc);
+  if (call->owned) {
+    delete call;
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(call->mu);
+    call->finished = true;
+  }
+  call->cv.notify_all();
+}
+
+static void call_fail(Call* call, int rc) {
+  call->rc = rc;
+  for (auto& x : call->code)
+    if (x == 2) x = -BGV_E_DEVICE;
+  call_finish(call);
+}
+
+// host-side checks and layout, on the caller's thread
+static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets,
+                       int mode, int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user) {
+  call->t0 = std::chrono::steady_clock::now();
   if (c->closed) return -BGV_E_CLOSED;
   if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
   if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
-
-  std::shared_lock<std::shared_mutex> cache_lock(c->cache_mu);
-  // host-side argument checks that the reference raises before any crypto
-  std::vector<int32_t> code(njobs, 2);
-  for (size_t j = 0; j < njobs; ++j) {
-    const bgv_job& jb = jobs[j];
-    if ((size_t)jb.first_set + jb.n_sets > nsets) return -BGV_E_ARG;
-    if (jb.n_sets == 0) {
-      code[j] = -BGV_E_EMPTY_SET;
-      continue;
-    }
-    for (uint32_t k = 0; k < jb.n_sets && code[j] == 2; ++k) {
-      const bgv_set& s = sets[jb.first_set + k];
-      if (s.n_pk == 0)
-        code[j] = -BGV_E_EMPTY_AGGREGATE;
-      else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes))
-        return -BGV_E_ARG;
-      else if (s.pk_indices)
-        for (uint32_t q = 0; q < s.n_pk; ++q)
-          if (s.pk_indices[q] >= c->n_pubkeys) {
-            code[j] = -BGV_E_BAD_INDEX;
-            break;
-          }
+  call->jobs = jobs;
+  call->njobs = njobs;
+  call->sets = sets;
+  call->nsets = nsets;
+  call->mode = mode;
+  call->out = out;
+  call->stats_out = stats;
+  call->done = done;
+  call->user = user;
+  call->code.assign(njobs, 2);
+  {
+    std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+    // argument checks the reference raises before any crypto
+    for (size_t j = 0; j < njobs; ++j) {
+      const bgv_job& jb = jobs[j];
+      if ((size_t)jb.first_set + jb.n_sets > nsets) return -BGV_E_ARG;
+      if (jb.n_sets == 0) {
+        call->code[j] = -BGV_E_EMPTY_SET;
+        continue;
+      }
+      for (uint32_t k = 0; k < jb.n_sets && call->code[j] == 2; ++k) {
+        const bgv_set& s = sets[jb.first_set + k];
+        if (s.n_pk == 0)
+          call->code[j] = -BGV_E_EMPTY_AGGREGATE;
+        else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes))
+          return -BGV_E_ARG;
+        else if (s.pk_indices)
+          for (uint32_t q = 0; q < s.n_pk; ++q)
+            if (s.pk_indices[q] >= c->n_pubkeys) {
+              call->code[j] = -BGV_E_BAD_INDEX;
+              break;
+            }
+      }
     }
   }
-
-  // ---- pass 1: lay out every job; batchable jobs (worker mode) share groups ----
-  Layout L;
+  // pass-1 layout: non-batchable jobs own their groups; batchable jobs (worker mode) share
+  Layout& L = call->L;
   L.job_groups.resize(njobs);
   L.job_first_slot.assign(njobs, 0);
   Builder B(L);
-  std::vector<size_t> todo;
   for (size_t j = 0; j < njobs; ++j)
-    if (code[j] == 2) todo.push_back(j);
-  auto shared_job = [&](size_t j) { return mode == BGV_MODE_WORKER && jobs[j].batchable; };
-  for (size_t j : todo) {
-    if (shared_job(j)) continue;
+    if (call->code[j] == 2) call->todo.push_back(j);
+  for (size_t j : call->todo) {
+    if (call->shared_job(j)) continue;
     B.close_group();
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
     B.close_group();
   }
   B.close_group();
-  for (size_t j : todo) {
-    if (!shared_job(j)) continue;
+  for (size_t j : call->todo) {
+    if (!call->shared_job(j)) continue;
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
   }
+  B.pad_to_wave();
+  call->set_sig.assign(nsets, 0);
+  call->set_pk.assign(nsets, 0);
+  if (L.slots.empty()) {  // nothing for the device
+    call_finish(call);
+    return BGV_OK;
+  }
+  {
+    std::lock_guard<std::mutex> lk(c->qmu);
+    if (c->stop) return -BGV_E_CLOSED;
+    c->queue.push_back(call);
+  }
+  c->qcv.notify_one();
+  return BGV_OK;
+}
+
+// After pass 1: statuses, verdicts and the retry units of one call.
+static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, const int32_t* verdict) {
+  Layout& L = call->L;
   const uint32_t nslots = (uint32_t)L.slots.size(), ngroups = (uint32_t)L.groups.size();
-  std::vector<int32_t> ss(nslots, 0), ps(nslots, 0), verdict(ngroups, 0);
-  std::vector<int32_t> set_sig(nsets, 0), set_pk(nsets, 0);
-
-  if (nslots) {
-    std::vector<uint64_t> sc(nslots);
-    fill_scalars(c, sc.data(), nslots);
-    for (uint32_t i = 0; i < nslots; ++i) L.slots[i].scalar = sc[i];
-    auto dx = exec_acquire(c, c->rr++);
-    Device& d = *dx.first;
-    Exec& x = *dx.second;
-    struct Release {
-      bgv_ctx* c;
-      Device* d;
-      Exec* x;
-      ~Release() { exec_release(c, d, x); }
-    } rel{c, &d, &x};
-    bool prof;
-    {
-      std::lock_guard<std::mutex> lk(c->prof_mu);
-      prof = c->profile;
+  for (uint32_t i = 0; i < nslots; ++i)
+    if (L.slot_set[i] >= 0) {
+      call->set_sig[L.slot_set[i]] = ss[i];
+      call->set_pk[L.slot_set[i]] = ps[i];
+      call->st.sets_verified++;
     }
-    HIPCHK(hipSetDevice(d.id));
-    int rc = exec_reserve(x, nslots, std::max<uint32_t>(ngroups, (uint32_t)njobs), L.idx.size(), L.pkb.size());
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(x.d_slots, L.slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
-    HIPCHK(hipMemcpyAsync(x.d_groups, L.groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
-    if (!L.idx.empty())
-      HIPCHK(hipMemcpyAsync(x.d_idx, L.idx.data(), 4 * L.idx.size(), hipMemcpyHostToDevice, x.main));
-    if (!L.pkb.empty()) HIPCHK(hipMemcpyAsync(x.d_pkb, L.pkb.data(), L.pkb.size(), hipMemcpyHostToDevice, x.main));
-    bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
-    bgv_streams S{x.main, {x.aux[0], x.aux[1]}, x.fork, {x.join[0], x.join[1]}, prof ? x.kev : nullptr};
-    HIPCHK(hipEventRecord(x.ev0, x.main));
-    HIPCHK(bgv_launch_sets(b, S));
-    HIPCHK(bgv_launch_groups(b, S));
-    HIPCHK(hipEventRecord(x.ev1, x.main));
-    HIPCHK(hipMemcpyAsync(ss.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
-    HIPCHK(hipMemcpyAsync(ps.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
-    HIPCHK(hipMemcpyAsync(verdict.data(), b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.main));
-    HIPCHK(hipStreamSynchronize(x.main));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
-    st.device_ms += ms;
-    if (prof) prof_add(c, x, true, true);
-    st.device_groups += ngroups;
-    for (uint32_t i = 0; i < nslots; ++i)
-      if (L.slot_set[i] >= 0) {
-        set_sig[L.slot_set[i]] = ss[i];
-        set_pk[L.slot_set[i]] = ps[i];
-        st.sets_verified++;
-      }
-
-    // ---- verdicts; jobs in failing mixed groups are re-verified alone ----
-    std::vector<size_t> retry;
-    std::vector<char> group_retried(ngroups, 0);
-    for (size_t j : todo) {
-      int32_t pre = job_precheck(set_sig, set_pk, jobs[j]);
-      if (pre != 2) {
-        code[j] = pre;
-        continue;
-      }
-      bool ok = true, needs_retry = false;
-      for (uint32_t g : L.job_groups[j])
-        if (!verdict[g]) {
-          ok = false;
-          if (L.group_shared[g]) {
-            needs_retry = true;
-            group_retried[g] = 1;
-          }
-        }
-      if (needs_retry) {
-        retry.push_back(j);
-      } else {
-        code[j] = ok ? 1 : 0;
-        if (ok && shared_job(j)) st.batch_sigs_success += jobs[j].n_sets;
-      }
+  call->st.device_groups += ngroups;
+  std::vector<char> group_retried(ngroups, 0);
+  std::vector<int> unit_of_group(ngroups, -1);
+  std::vector<char> seen(call->njobs, 0);
+  for (size_t j : call->todo) {
+    const int32_t pre = job_precheck(call->set_sig, call->set_pk, call->jobs[j]);
+    if (pre != 2) {
+      call->code[j] = pre;
+      continue;
     }
-    for (char r : group_retried) st.batch_retries += r;
-
-    // ---- pass 2: per-job groups over the per-slot results already on the device.
-    // Each retried job gets its own final exponentiation: the same equation as
-    // verifying the job alone, with the same nonzero randomizers.
-    if (!retry.empty()) {
-      std::vector<bgv_dgroup> rg;
-      std::vector<std::vector<uint32_t>> jg(retry.size());
-      for (size_t q = 0; q < retry.size(); ++q) {
-        const size_t j = retry[q];
-        for (uint32_t off = 0; off < jobs[j].n_sets; off += BGV_WAVE) {
-          jg[q].push_back((uint32_t)rg.size());
-          rg.push_back(bgv_dgroup{L.job_first_slot[j] + off, std::min<uint32_t>(BGV_WAVE, jobs[j].n_sets - off)});
-        }
+    bool ok = true;
+    int first_bad_shared = -1;
+    for (uint32_t g : L.job_groups[j])
+      if (!verdict[g]) {
+        ok = false;
+        if (L.group_shared[g] && first_bad_shared < 0) first_bad_shared = (int)g;
       }
-      const uint32_t nrg = (uint32_t)rg.size();
-      if (nrg > x.group_cap) {
-        rc = exec_reserve(x, nslots, nrg, L.idx.size(), L.pkb.size());
-        if (rc) return rc;
+    if (first_bad_shared >= 0) {
+      group_retried[first_bad_shared] = 1;
+      if (unit_of_group[first_bad_shared] < 0) {
+        unit_of_group[first_bad_shared] = (int)call->units.size();
+        call->units.emplace_back();
       }
-      std::vector<int32_t> rv(nrg, 0);
-      HIPCHK(hipMemcpyAsync(x.d_groups, rg.data(), sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.main));
-      b = make_batch(d, x, nslots, nrg);
-      HIPCHK(hipEventRecord(x.ev0, x.main));
-      HIPCHK(bgv_launch_groups(b, S));
-      HIPCHK(hipEventRecord(x.ev1, x.main));
-      HIPCHK(hipMemcpyAsync(rv.data(), b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.main));
-      HIPCHK(hipStreamSynchronize(x.main));
-      HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
-      st.device_ms += ms;
-      if (prof) prof_add(c, x, false, true);
-      st.device_groups += nrg;
-      for (size_t q = 0; q < retry.size(); ++q) {
-        bool ok = true;
-        for (uint32_t g : jg[q]) ok = ok && rv[g];
-        code[retry[q]] = ok ? 1 : 0;
+      if (!seen[j]) {
+        seen[j] = 1;
+        call->units[unit_of_group[first_bad_shared]].push_back(j);
       }
+    } else {
+      call->code[j] = ok ? 1 : 0;
+      if (ok && call->shared_job(j)) call->st.batch_sigs_success += call->jobs[j].n_sets;
     }
   }
-  for (size_t j = 0; j < njobs; ++j) out[j] = code[j] == 2 ? -BGV_E_DEVICE : code[j];
-  st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (stats) *stats = st;
+  for (char r : group_retried) call->st.batch_retries += r;
+}
+
+// Group testing for one retry round: split every pending unit into parts.
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg) {
+  call->parts.clear();
+  for (const auto& u : call->units) {
+    const size_t k = std::min<size_t>(retry_fanout(), u.size());
+    for (size_t p = 0; p < k; ++p) {
+      Part part;
+      const size_t lo = u.size() * p / k, hi = u.size() * (p + 1) / k;
+      part.jobs.assign(u.begin() + lo, u.begin() + hi);
+      for (size_t q = 0; q < part.jobs.size();) {  // maximal runs of consecutive slots
+        const uint32_t first = call->L.job_first_slot[part.jobs[q]];
+        uint32_t n = 0;
+        size_t q2 = q;
+        while (q2 < part.jobs.size() && call->L.job_first_slot[part.jobs[q2]] == first + n) {
+          n += call->jobs[part.jobs[q2]].n_sets;
+          ++q2;
+        }
+        for (uint32_t off = 0; off < n; off += BGV_WAVE) {
+          part.groups.push_back((uint32_t)rg.size());
+          rg.push_back(bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off)});
+        }
+        q = q2;
+      }
+      call->parts.push_back(std::move(part));
+    }
+  }
+  call->units.clear();
+}
+
+static void call_after_round(Call* call, const int32_t* rv) {
+  call->st.device_groups += 0;
+  for (const Part& part : call->parts) {
+    bool ok = true;
+    for (uint32_t g : part.groups) ok = ok && rv[g];
+    if (ok || part.jobs.size() == 1) {
+      for (size_t j : part.jobs) call->code[j] = ok ? 1 : 0;
+    } else {
+      call->units.push_back(part.jobs);
+    }
+  }
+  call->parts.clear();
+}
+
+// Run one merged super-batch of calls on one dispatcher's stream.
+static bool trace_on() {
+  static const bool v = getenv("BGV_TRACE") != nullptr;
+  return v;
+}
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) {
+  const auto tb = std::chrono::steady_clock::now();
+  double t_merge = 0, t_tok = 0, t_sets = 0, t_pass1 = 0, t_post = 0, t_retry = 0;
+  // merge the calls' layouts
+  uint32_t nslots = 0, ngroups = 0;
+  size_t nidx = 0, npkb = 0;
+  for (Call* call : calls) {
+    call->slot_base = nslots;
+    nslots += (uint32_t)call->L.slots.size();
+    ngroups += (uint32_t)call->L.groups.size();
+    nidx += call->L.idx.size();
+    npkb += call->L.pkb.size();
+  }
+  std::vector<bgv_dslot> slots;
+  slots.reserve(nslots);
+  std::vector<bgv_dgroup> groups;
+  groups.reserve(ngroups);
+  std::vector<uint32_t> idx;
+  idx.reserve(nidx);
+  std::vector<uint8_t> pkb;
+  pkb.reserve(npkb);
+  for (Call* call : calls) {
+    const uint32_t ib = (uint32_t)idx.size(), pb = (uint32_t)(pkb.size() / 96), gb = (uint32_t)groups.size();
+    for (bgv_dslot s : call->L.slots) {
+      if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
+      if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
+      if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
+      slots.push_back(s);
+    }
+    for (bgv_dgroup g : call->L.groups) groups.push_back(bgv_dgroup{g.first_slot + call->slot_base, g.n_slots});
+    idx.insert(idx.end(), call->L.idx.begin(), call->L.idx.end());
+    pkb.insert(pkb.end(), call->L.pkb.begin(), call->L.pkb.end());
+  }
+  std::vector<uint64_t> sc(nslots);
+  fill_scalars(c, sc.data(), nslots);
+  for (uint32_t i = 0; i < nslots; ++i) slots[i].scalar = sc[i];
+
+  bool prof;
+  {
+    std::lock_guard<std::mutex> lk(c->prof_mu);
+    prof = c->profile;
+  }
+  t_merge = ms_since(tb);
+  HIPCHK(hipSetDevice(d.id));
+  int rc;
+  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
+      (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1))) ||
+      (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
+    return rc;
+  HIPCHK(hipMemcpyAsync(x.d_slots, slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
+  HIPCHK(hipMemcpyAsync(x.d_groups, groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
+  if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, idx.data(), 4 * nidx, hipMemcpyHostToDevice, x.main));
+  if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, pkb.data(), npkb, hipMemcpyHostToDevice, x.main));
+  bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
+  bgv_streams S{x.main, prof ? x.kev : nullptr};
+  bgv_streams SC{x.close, prof ? x.kev : nullptr};
+  std::vector<int32_t> ss(nslots), ps(nslots), verdict(ngroups);
+  {
+    // One super-batch at a time runs the compute-bound per-set kernels; the
+    // latency-bound group closing of one batch then overlaps the next batch's
+    // per-set kernels (dispatchers stagger instead of running in lockstep).
+    const auto tt = std::chrono::steady_clock::now();
+    std::unique_lock<std::mutex> tok(*d.compute_mu);
+    t_tok = ms_since(tt);
+    HIPCHK(hipEventRecord(x.ev0, x.main));
+    HIPCHK(bgv_launch_sets(b, S));
+    HIPCHK(hipEventRecord(x.ev_sets, x.main));
+    HIPCHK(hipEventSynchronize(x.ev_sets));
+    t_sets = ms_since(tt) - t_tok;
+  }
+  const auto tg = std::chrono::steady_clock::now();
+  HIPCHK(bgv_launch_groups(b, SC));
+  HIPCHK(hipEventRecord(x.ev1, x.close));
+  HIPCHK(hipMemcpyAsync(ss.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipMemcpyAsync(ps.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipMemcpyAsync(verdict.data(), b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipStreamSynchronize(x.close));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+  if (prof) prof_add(c, x, true, true);
+  t_pass1 = ms_since(tg);
+  const auto tp = std::chrono::steady_clock::now();
+  {
+    uint32_t gb = 0;
+    for (Call* call : calls) {
+      call->st.device_ms += ms;
+      call_after_pass1(call, ss.data() + call->slot_base, ps.data() + call->slot_base, verdict.data() + gb);
+      gb += (uint32_t)call->L.groups.size();
+    }
+  }
+  t_post = ms_since(tp);
+  const auto tr = std::chrono::steady_clock::now();
+  int rounds = 0;
+  // retry rounds over the per-slot results on the device
+  for (;;) {
+    std::vector<bgv_dgroup> rg;
+    std::vector<uint32_t> base;
+    for (Call* call : calls) {
+      base.push_back((uint32_t)rg.size());
+      call_build_parts(call, rg);
+    }
+    if (rg.empty()) break;
+    ++rounds;
+    const uint32_t nrg = (uint32_t)rg.size();
+    if ((rc = exec_reserve_groups(x, nrg))) return rc;
+    std::vector<int32_t> rv(nrg);
+    HIPCHK(hipMemcpyAsync(x.d_groups, rg.data(), sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
+    b = make_batch(d, x, nslots, nrg);
+    HIPCHK(hipEventRecord(x.ev0, x.close));
+    HIPCHK(bgv_launch_groups(b, SC));
+    HIPCHK(hipEventRecord(x.ev1, x.close));
+    HIPCHK(hipMemcpyAsync(rv.data(), b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
+    HIPCHK(hipStreamSynchronize(x.close));
+    HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+    if (prof) prof_add(c, x, false, true);
+    for (size_t k = 0; k < calls.size(); ++k) {
+      Call* call = calls[k];
+      call->st.device_ms += ms;
+      uint32_t mine = 0;
+      for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
+      call->st.device_groups += mine;
+      // part group indices are global to this round
+      call_after_round(call, rv.data());
+    }
+  }
+  t_retry = ms_since(tr);
+  if (trace_on())
+    fprintf(stderr,
+            "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
+            "retry(%d) %.1f total %.1f ms\n",
+            d.id, calls.size(), nslots, ngroups, t_merge, t_tok, t_sets, t_pass1, t_post, rounds, t_retry, ms_since(tb));
   return BGV_OK;
+}
+
+static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
+  for (;;) {
+    std::vector<Call*> calls;
+    {
+      std::unique_lock<std::mutex> lk(c->qmu);
+      c->qcv.wait(lk, [c] { return c->stop || !c->queue.empty(); });
+      if (c->queue.empty()) return;
+      // Coalescing window: a super-batch costs about the same device time from a
+      // few thousand to ~10^5 sets (its closing phases are latency-bound), so give
+      // concurrent callers a moment to join before launching.
+      auto queued_slots = [c] {
+        size_t n = 0;
+        for (Call* q : c->queue) n += q->L.slots.size();
+        return n;
+      };
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_us());
+      while (!c->stop && queued_slots() < max_batch_slots() &&
+             c->qcv.wait_until(lk, until) != std::cv_status::timeout) {
+      }
+      if (c->queue.empty()) continue;
+      size_t slots = 0;
+      while (!c->queue.empty()) {
+        Call* call = c->queue.front();
+        const size_t n = call->L.slots.size();
+        if (!calls.empty() && slots + n > max_batch_slots()) break;
+        calls.push_back(call);
+        slots += n;
+        c->queue.pop_front();
+      }
+      if (!c->queue.empty()) c->qcv.notify_one();
+    }
+    int rc;
+    {
+      std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+      rc = run_batch(c, *d, *x, calls);
+    }
+    for (Call* call : calls) {
+      if (rc != BGV_OK)
+        call_fail(call, rc);
+      else
+        call_finish(call);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -525,33 +777,11 @@ static int verify_impl(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_
 // ---------------------------------------------------------------------------
 extern "C" {
 
-int bgv_device_count(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-  return n;
-}
-
-static void worker_loop(bgv_ctx* c) {
-  for (;;) {
-    Job jb;
-    {
-      std::unique_lock<std::mutex> lk(c->qmu);
-      c->qcv.wait(lk, [c] { return c->stop || !c->queue.empty(); });
-      if (c->queue.empty()) return;
-      jb = c->queue.front();
-      c->queue.pop_front();
-    }
-    int rc = verify_impl(c, jb.jobs, jb.njobs, jb.sets, jb.nsets, jb.mode, jb.out, jb.stats);
-    if (jb.done) jb.done(jb.user, rc);
-  }
-}
-
 static void ctx_free_devices(bgv_ctx* c) {
   for (Device& d : c->devs) {
     (void)hipSetDevice(d.id);
-    for (Exec* x : d.all_execs) exec_destroy(x);
-    d.all_execs.clear();
-    d.free_execs.clear();
+    for (Exec* x : d.execs) exec_destroy(x);
+    d.execs.clear();
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
@@ -573,10 +803,9 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     d.id = (devices && ndev > 0) ? devices[i] : 0;
     bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
               hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
-    for (int k = 0; ok && k < BGV_EXECS_PER_DEVICE; ++k) {
+    for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
       Exec* x = new Exec();
-      d.all_execs.push_back(x);
-      d.free_execs.push_back(x);
+      d.execs.push_back(x);
       ok = exec_create(x) == BGV_OK;
     }
     if (!ok) {
@@ -585,7 +814,8 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
       return d.id < 0 || d.id >= avail ? -BGV_E_ARG : -BGV_E_DEVICE;
     }
   }
-  for (int k = 0; k < n * BGV_EXECS_PER_DEVICE; ++k) c->workers.emplace_back(worker_loop, c);
+  for (Device& d : c->devs)
+    for (Exec* x : d.execs) c->dispatchers.emplace_back(dispatcher_loop, c, &d, x);
   *out = c;
   return BGV_OK;
 }
@@ -597,9 +827,9 @@ int bgv_close(bgv_ctx* c) {
     c->stop = true;
   }
   c->qcv.notify_all();
-  for (auto& w : c->workers)
+  for (auto& w : c->dispatchers)
     if (w.joinable()) w.join();
-  c->workers.clear();
+  c->dispatchers.clear();
   std::unique_lock<std::shared_mutex> lk(c->cache_mu);
   if (c->closed.exchange(true)) return BGV_OK;
   ctx_free_devices(c);
@@ -687,20 +917,25 @@ int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, i
 int bgv_verify(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
                int32_t* out, bgv_stats* stats) {
   if (!c) return -BGV_E_ARG;
-  return verify_impl(c, jobs, njobs, sets, nsets, mode, out, stats);
+  Call* call = new Call();
+  int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, nullptr, nullptr);
+  if (rc == BGV_OK) {
+    std::unique_lock<std::mutex> lk(call->mu);
+    call->cv.wait(lk, [call] { return call->finished; });
+    rc = call->rc;
+  }
+  delete call;
+  return rc;
 }
 
 int bgv_verify_async(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
                      int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user) {
   if (!c) return -BGV_E_ARG;
-  if (c->closed) return -BGV_E_CLOSED;
-  {
-    std::lock_guard<std::mutex> lk(c->qmu);
-    if (c->stop) return -BGV_E_CLOSED;
-    c->queue.push_back(Job{jobs, njobs, sets, nsets, mode, out, stats, done, user});
-  }
-  c->qcv.notify_one();
-  return BGV_OK;
+  Call* call = new Call();
+  call->owned = true;  // deleted by the dispatcher after done()
+  int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, done, user);
+  if (rc != BGV_OK) delete call;
+  return rc;
 }
 
 int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out96[96]) {

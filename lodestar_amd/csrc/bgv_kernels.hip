@@ -22,10 +22,8 @@
 
 extern "C" {
 
-__global__ void __launch_bounds__(64) k_sig(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                            g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nslots) return;
+__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
+                                      int32_t* __restrict__ sig_status) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
   g2_jac out = jac_infinity<fp2_t>();
@@ -55,10 +53,7 @@ __global__ void __launch_bounds__(64) k_sig(const bgv_dslot* __restrict__ slots,
   sig_status[s] = st;
 }
 
-__global__ void __launch_bounds__(64) k_hash(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                             g2_aff* __restrict__ h) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nslots) return;
+__device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* __restrict__ h) {
   const bgv_dslot& d = slots[s];
   if (d.flags & BGV_SLOT_PAD) return;
   uint8_t msg[32];
@@ -68,12 +63,10 @@ __global__ void __launch_bounds__(64) k_hash(const bgv_dslot* __restrict__ slots
   h[s] = a;
 }
 
-__global__ void __launch_bounds__(64) k_pk(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                           const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                           const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                           int32_t* __restrict__ pk_status) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nslots) return;
+__device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
+                                     const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                     const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                     int32_t* __restrict__ pk_status) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
   if (d.flags & BGV_SLOT_PAD) {
@@ -107,6 +100,24 @@ __global__ void __launch_bounds__(64) k_pk(const bgv_dslot* __restrict__ slots, 
       st = BGV_ST_INFINITY;
   }
   pk_status[s] = st;
+}
+
+// The three independent per-set tasks in one launch (blockIdx.y = task), so one
+// batch keeps 3x the wavefronts in flight on a single stream.
+__global__ void __launch_bounds__(64) k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                             g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status,
+                                             g2_aff* __restrict__ h, const uint32_t* __restrict__ pk_idx,
+                                             const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
+                                             g1_aff* __restrict__ rpk, int32_t* __restrict__ pk_status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  // hash first: the longest task starts earliest
+  if (blockIdx.y == 0)
+    task_hash(s, slots, h);
+  else if (blockIdx.y == 1)
+    task_sig(s, slots, rsig, sig_status);
+  else
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status);
 }
 
 __global__ void __launch_bounds__(64) k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
@@ -157,14 +168,22 @@ __global__ void __launch_bounds__(64) k_reduce(const bgv_dgroup* __restrict__ gr
   }
 }
 
-__global__ void __launch_bounds__(64) k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
-                                              const g2_jac* __restrict__ sg, int32_t* __restrict__ verdict) {
+// Group closing, split in two launches to keep each kernel's stack small:
+//   k_final_ml   f_g *= MillerLoop(-G1, sum r_i sig_i)
+//   k_final      final exponentiation of f_g, verdict = (result == 1)
+__global__ void __launch_bounds__(64) k_final_ml(uint32_t ngroups, fp12_t* __restrict__ fg,
+                                                 const g2_jac* __restrict__ sg) {
   const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= ngroups) return;
-  fp12_t f = fg[gi];
   g2_aff sa;
-  if (jac_to_aff(&sa, sg[gi])) f = fp12_mul(f, miller_loop(g1_neg_generator(), sa));
-  verdict[gi] = fp12_is_one(final_exp(f)) ? 1 : 0;
+  if (jac_to_aff(&sa, sg[gi])) fg[gi] = fp12_mul(fg[gi], miller_loop(g1_neg_generator(), sa));
+}
+
+__global__ void __launch_bounds__(64) k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
+                                              int32_t* __restrict__ verdict) {
+  const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= ngroups) return;
+  verdict[gi] = fp12_is_one(final_exp(fg[gi])) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -277,36 +296,21 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 
-// Per-set kernels.  k_sig, k_hash and k_pk are independent and run concurrently
-// on three streams (3x the wavefronts in flight of one set per lane); k_miller
-// joins them on the main stream.
+// Per-set kernels on one stream: k_prep (sig / hash / pk tasks side by side),
+// then k_miller.  Kernel k is bracketed by events kev[2k], kev[2k+1] when profiling.
+#define BGV_MARK(i) \
+  if (s.kev) (void)hipEventRecord(s.kev[i], s.main)
 hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
-  hipEvent_t* ev = s.kev;  // optional: [2k] start / [2k+1] end of kernel k
-#define BGV_MARK(i, st) \
-  if (ev) (void)hipEventRecord(ev[i], st)
-  (void)hipEventRecord(s.fork, s.main);
-  (void)hipStreamWaitEvent(s.aux[0], s.fork, 0);
-  (void)hipStreamWaitEvent(s.aux[1], s.fork, 0);
-  BGV_MARK(0, s.aux[0]);
-  hipLaunchKernelGGL(k_sig, dim3(nblk(n, 64)), dim3(64), 0, s.aux[0], b.slots, n, b.rsig, b.sig_status);
-  BGV_MARK(1, s.aux[0]);
-  BGV_MARK(2, s.main);
-  hipLaunchKernelGGL(k_hash, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.h);
-  BGV_MARK(3, s.main);
-  BGV_MARK(4, s.aux[1]);
-  hipLaunchKernelGGL(k_pk, dim3(nblk(n, 64)), dim3(64), 0, s.aux[1], b.slots, n, b.pk_idx,
-                     reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status);
-  BGV_MARK(5, s.aux[1]);
-  (void)hipEventRecord(s.join[0], s.aux[0]);
-  (void)hipEventRecord(s.join[1], s.aux[1]);
-  (void)hipStreamWaitEvent(s.main, s.join[0], 0);
-  (void)hipStreamWaitEvent(s.main, s.join[1], 0);
-  BGV_MARK(6, s.main);
+  BGV_MARK(0);
+  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
+                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status);
+  BGV_MARK(1);
+  BGV_MARK(2);
   hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
                      b.pk_status, b.f);
-  BGV_MARK(7, s.main);
+  BGV_MARK(3);
   return hipGetLastError();
 }
 
@@ -314,18 +318,20 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
 // the first pass and, over the same per-slot results, for the per-job retry pass.
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
   if (b.ngroups == 0) return hipSuccess;
-  hipEvent_t* ev = s.kev;
   const size_t lds = BGV_WAVE * (sizeof(fp12_t) + sizeof(g2_jac));
-  BGV_MARK(8, s.main);
+  BGV_MARK(4);
   hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.rsig, b.sig_status,
                      b.pk_status, b.fg, b.sg);
-  BGV_MARK(9, s.main);
-  BGV_MARK(10, s.main);
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.sg, b.verdict);
-  BGV_MARK(11, s.main);
-#undef BGV_MARK
+  BGV_MARK(5);
+  BGV_MARK(6);
+  hipLaunchKernelGGL(k_final_ml, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.sg);
+  BGV_MARK(7);
+  BGV_MARK(8);
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.verdict);
+  BGV_MARK(9);
   return hipGetLastError();
 }
+#undef BGV_MARK
 
 size_t bgv_slot_bytes() {
   return sizeof(g2_jac) + sizeof(g2_aff) + sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);

@@ -41,11 +41,11 @@ struct bgv_dev_batch {
 };
 
 // kernels of one verify launch, in order (names for per-kernel timing)
-#define BGV_NKERNELS 6
-static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_sig", "k_hash", "k_pk", "k_miller", "k_reduce", "k_final"};
+#define BGV_NKERNELS 5
+#define BGV_NSETKERNELS 2  // the first BGV_NSETKERNELS run once per call (bgv_launch_sets)
+static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_prep", "k_miller", "k_reduce", "k_final_ml", "k_final"};
 struct bgv_streams {
-  hipStream_t main, aux[2];
-  hipEvent_t fork, join[2];
+  hipStream_t main;
   hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr
 };
 hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);

@@ -70,6 +70,12 @@ void hs_k_final_body(const uint8_t* f, const uint8_t* s_aff) {
   fp12_t x = fp12_mul(in_fp12(f), miller_loop(g1_neg_generator(), in_g2(s_aff)));
   (void)fp12_is_one(final_exp(x));
 }
+void hs_k_final_ml_body(const uint8_t* f, const uint8_t* s_aff) {
+  g2_aff sa;
+  (void)jac_to_aff(&sa, jac_from_aff(in_g2(s_aff)));
+  (void)fp12_mul(in_fp12(f), miller_loop(g1_neg_generator(), sa));
+}
+void hs_k_final_exp_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
 void hs_k_reduce_step(const uint8_t* f, const uint8_t* s_aff) {
   (void)fp12_mul(in_fp12(f), in_fp12(f));
   (void)jac_add(jac_from_aff(in_g2(s_aff)), jac_dbl(jac_from_aff(in_g2(s_aff))));

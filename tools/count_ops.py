@@ -60,6 +60,8 @@ def main():
     out["k_miller"] = list(count(lambda: L.hs_k_miller_body(hs.g1_b(pk), hs.g2_b(h))))
     f12 = hs.fp12_b_tower([rng.randrange(o.P) for _ in range(12)])
     out["k_final[per group]"] = list(count(lambda: L.hs_k_final_body(f12, hs.g2_b(sig))))
+    out["k_final_ml[per group]"] = list(count(lambda: L.hs_k_final_ml_body(f12, hs.g2_b(sig))))
+    out["k_final_exp[per group]"] = list(count(lambda: L.hs_k_final_exp_body(f12)))
     out["k_reduce[per tree step]"] = list(count(lambda: L.hs_k_reduce_step(f12, hs.g2_b(sig))))
     res = {
         "note": "Fp products [mul, sqr] per set (per group / per tree step where named), counted in the "
