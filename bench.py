@@ -205,9 +205,11 @@ def main():
         # its overlap with the other in-flight batches)
         avg = {k: v / max(1, launches) for k, v in kms.items()}
         dom = max(per_set, key=lambda k: avg.get(k, 0))
-        # sets launched per verify call (first pass + retries), averaged
+        # sets per verify call, and per launch of the per-set kernels (calls are merged
+        # into device super-batches, so one launch covers several calls)
         slots = statistics.mean(s.sets_verified for s in stats)
-        achieved = per_set[dom] * MACS_PER_FP_MUL * slots / (avg[dom] * 1e-3)
+        slots_per_launch = sum(s.sets_verified for s in stats) / max(1, launches)
+        achieved = per_set[dom] * MACS_PER_FP_MUL * slots_per_launch / (avg[dom] * 1e-3)
         # whole-pipeline VALU figure: every verify kernel's counted work over the step time
         per_group = opc["k_final_ml[per group]"] + opc["k_final_exp[per group]"]
         groups = statistics.mean(s.device_groups for s in stats)
@@ -245,6 +247,7 @@ def main():
             "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
                          "unit": "TMAC/s (u32 mad)", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
                          "work_per_set": "%d Fp-mul-eq x %d MAC" % (per_set[dom], MACS_PER_FP_MUL),
+                         "sets_per_launch": slots_per_launch, "ms_per_launch": avg[dom],
                          "pipeline_frac": pipeline_frac},
             "setup_s": setup_s,
         }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box script: parity tests, smoke, bench, rocprof kernel-trace summary.
+# GPU-box script: parity tests, smoke, default bench (with cpu_baseline), rocprof kernel-trace summary.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,11 +8,9 @@ timeout -k 10 300 python -u -m pytest tests/ -m gpu -x -v --timeout 240 --timeou
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-for inf in ${INFLIGHT:-1 4 8}; do
-  timeout -k 10 300 python bench.py --steps ${STEPS:-8} --warmup 1 --inflight $inf --no-cpu-baseline > gpurun_out/bench_inf$inf.json 2> gpurun_out/bench_inf$inf.err || exit $?
-  cat gpurun_out/bench_inf$inf.json
-done
+timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
+cat gpurun_out/bench_$TAG.json
 if [ -n "$PROF" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --inflight 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --no-cpu-baseline > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_bench_$TAG.err || exit $?
   find gpurun_out/prof_$TAG -name "*stats*" | head
 fi
