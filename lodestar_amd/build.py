@@ -49,5 +49,31 @@ def build(force=False, verbose=True):
     return LIB
 
 
+NODE_DIR = os.path.join(HERE, "node")
+NODE_SRC = os.path.join(NODE_DIR, "blsgpu_napi.c")
+NODE_ADDON = os.path.join(NODE_DIR, "blsgpu.node")
+NODE_INCLUDE = os.environ.get("NODE_INCLUDE", "/usr/include/node")
+
+
+def build_node(force=False, verbose=True):
+    """N-API addon (lodestar_amd/node/blsgpu.node) over libblsgpu.so; None when the image has
+    no Node headers.  Built with gcc: the addon is plain C over the C-ABI."""
+    if not os.path.exists(os.path.join(NODE_INCLUDE, "node_api.h")):
+        return None
+    build(verbose=verbose)
+    srcs = [NODE_SRC, LIB, os.path.join(HERE, "..", "include", "blsgpu.h")]
+    if not force and os.path.exists(NODE_ADDON) and all(
+            os.path.getmtime(NODE_ADDON) >= os.path.getmtime(d) for d in srcs):
+        return NODE_ADDON
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-I" + NODE_INCLUDE, NODE_SRC, "-L" + HERE, "-lblsgpu",
+           "-Wl,-rpath,$ORIGIN/..", "-o", NODE_ADDON + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(NODE_ADDON + ".tmp", NODE_ADDON)
+    return NODE_ADDON
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_node(force="--force" in sys.argv)

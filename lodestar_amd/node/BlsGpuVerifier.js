@@ -1,0 +1,172 @@
+"use strict";
+/**
+ * BlsGpuVerifier — IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:20-46) on MI355X.
+ *
+ * Drop-in beside BlsMultiThreadWorkerPool (chain/bls/multithread/index.ts:98-424): the same
+ * verifySignatureSets(sets, opts) -> Promise<boolean> and close() -> Promise<void>, the same
+ * batchable buffering (index.ts:238-285, 406-412), 128-set jobs (index.ts:39,155-166) and
+ * QUEUE_ABORTED after close (index.ts:176-197, 239-241).  Per-job verification, batching and
+ * retry run on the GPU (libblsgpu, BGV_MODE_WORKER), so every job's verdict matches the worker's.
+ *
+ * Pubkeys are validator indices into the device-resident cache (SURVEY §7 "pubkey identity at
+ * the boundary", option (a)): set.pubkey / set.pubkeys hold numbers (or {index}).
+ */
+const path = require("path");
+const addon = require(path.join(__dirname, "blsgpu.node"));
+
+const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:39
+const MAX_BUFFERED_SIGS = 32; // index.ts:48 (the GPU prefers larger; see opts)
+const MAX_BUFFER_WAIT_MS = 100; // index.ts:57
+
+const SignatureSetType = {single: "single", aggregate: "aggregate"};
+
+class QueueError extends Error {
+  constructor(code) {
+    super(code);
+    this.type = {code};
+  }
+}
+
+/** chain/bls/multithread/utils.ts:4-19 */
+function chunkifyMaximizeChunkSize(arr, minPerChunk) {
+  const chunkCount = Math.floor(arr.length / minPerChunk);
+  if (chunkCount <= 1) return [arr];
+  const perChunk = Math.ceil(arr.length / chunkCount);
+  const out = [];
+  for (let i = 0; i < arr.length; i += perChunk) out.push(arr.slice(i, i + perChunk));
+  return out;
+}
+
+/** chain/bls/utils.ts:18-26 */
+function getAggregatedPubkeysCount(sets) {
+  let n = 0;
+  for (const s of sets) if (s.type === SignatureSetType.aggregate) n += s.pubkeys.length;
+  return n;
+}
+
+function indexOf(pk) {
+  return typeof pk === "number" ? pk : pk.index;
+}
+
+// A pubkey is a validator index (a number, or a PublicKey tagged with .index by the
+// Index2PubkeyCache, INTEGRATION.md), else its 96-B uncompressed bytes (pk.toBytes(false)
+// for @chainsafe/bls keys outside the cache, e.g. deposits).
+function uncompressed(pk) {
+  if (pk instanceof Uint8Array) return pk;
+  return pk.toBytes(false);
+}
+
+function toNativeSet(s) {
+  let pks;
+  if (s.type === SignatureSetType.single) pks = [s.pubkey];
+  else if (s.type === SignatureSetType.aggregate) pks = s.pubkeys;
+  else throw Error("Unknown signature set type");
+  if (pks.every((pk) => indexOf(pk) !== undefined)) {
+    return {pkIndices: Uint32Array.from(pks, indexOf), msg: s.signingRoot, sig: s.signature};
+  }
+  const bytes = new Uint8Array(96 * pks.length);
+  pks.forEach((pk, i) => bytes.set(uncompressed(pk), 96 * i));
+  return {pkBytes: bytes, msg: s.signingRoot, sig: s.signature};
+}
+
+class BlsGpuVerifier {
+  constructor(opts = {}, modules = {}) {
+    this.metrics = modules.metrics || null;
+    this.ctx = opts.ctx || addon.init(opts.devices || []);
+    this.blsVerifyAllMultiThread = opts.blsVerifyAllMultiThread || false;
+    this.maxBufferedSigs = opts.maxBufferedSigs || MAX_BUFFERED_SIGS;
+    this.maxBufferWaitMs = opts.maxBufferWaitMs || MAX_BUFFER_WAIT_MS;
+    this.jobs = [];
+    this.bufferedJobs = null;
+    this.closed = false;
+    this.counters = {aggregatedPubkeys: 0, batchRetries: 0, successJobsSignatureSetsCount: 0, errorJobsSignatureSetsCount: 0};
+  }
+
+  async verifySignatureSets(sets, opts = {}) {
+    this.counters.aggregatedPubkeys += getAggregatedPubkeysCount(sets);
+    if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
+      // index.ts:138-151: one job verified at once (no buffering)
+      const codes = await addon.verify(this.ctx, [{sets: sets.map(toNativeSet), batchable: false}], 1);
+      return unwrap(codes[0]);
+    }
+    const results = await Promise.all(
+      chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) =>
+        this.queueBlsWork({opts, sets: chunk.map(toNativeSet)})
+      )
+    );
+    if (results.length === 0) throw Error("Empty results array");
+    return results.every((v) => v === true);
+  }
+
+  async close() {
+    if (this.bufferedJobs) clearTimeout(this.bufferedJobs.timeout);
+    const pending = this.jobs.concat(this.bufferedJobs ? this.bufferedJobs.jobs : []);
+    for (const job of pending) job.reject(new QueueError("QUEUE_ABORTED"));
+    this.jobs = [];
+    this.bufferedJobs = null;
+    this.closed = true;
+    addon.close(this.ctx);
+  }
+
+  queueBlsWork(workReq) {
+    if (this.closed) return Promise.reject(new QueueError("QUEUE_ABORTED"));
+    return new Promise((resolve, reject) => {
+      const job = {resolve, reject, workReq};
+      if (workReq.opts.batchable) {
+        if (!this.bufferedJobs) {
+          this.bufferedJobs = {jobs: [], sigCount: 0, timeout: setTimeout(this.runBufferedJobs, this.maxBufferWaitMs)};
+        }
+        this.bufferedJobs.jobs.push(job);
+        this.bufferedJobs.sigCount += workReq.sets.length;
+        if (this.bufferedJobs.sigCount > this.maxBufferedSigs) {
+          clearTimeout(this.bufferedJobs.timeout);
+          this.runBufferedJobs();
+        }
+      } else {
+        this.jobs.push(job);
+        setTimeout(this.runJob, 0);
+      }
+    });
+  }
+
+  runBufferedJobs = () => {
+    if (this.bufferedJobs) {
+      this.jobs.push(...this.bufferedJobs.jobs);
+      this.bufferedJobs = null;
+      setTimeout(this.runJob, 0);
+    }
+  };
+
+  // All queued jobs go to the device in one call; the library merges concurrent calls into
+  // super-batches, so there is no idle-worker bookkeeping here (index.ts:290-381).
+  runJob = async () => {
+    if (this.closed || this.jobs.length === 0) return;
+    const jobs = this.jobs.splice(0, this.jobs.length);
+    try {
+      const codes = await addon.verify(
+        this.ctx,
+        jobs.map((j) => ({sets: j.workReq.sets, batchable: Boolean(j.workReq.opts.batchable)})),
+        0
+      );
+      jobs.forEach((job, i) => {
+        const c = codes[i];
+        if (c < 0) {
+          this.counters.errorJobsSignatureSetsCount += job.workReq.sets.length;
+          job.reject(Error(addon.strerror(-c)));
+        } else {
+          this.counters.successJobsSignatureSetsCount += job.workReq.sets.length;
+          job.resolve(c === 1);
+        }
+      });
+    } catch (e) {
+      for (const job of jobs) job.reject(e);
+    }
+  };
+}
+
+function unwrap(code) {
+  if (code < 0) throw Error(addon.strerror(-code));
+  return code === 1;
+}
+
+module.exports = {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, getAggregatedPubkeysCount, addon};

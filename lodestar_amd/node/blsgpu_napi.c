@@ -1,0 +1,310 @@
+/*
+ * blsgpu.node — N-API binding of libblsgpu.so for Node (the reference's own runtime).
+ *
+ * Exposes the C-ABI (include/blsgpu.h) to JavaScript; BlsGpuVerifier.js builds the
+ * IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:20-46) on top.
+ * Verification runs in napi_async_work on the libuv pool and resolves a Promise on
+ * the main thread, like the reference's worker round trip (multithread/index.ts:290-381).
+ *
+ *   init(devices?: number[]) -> ctx
+ *   pubkeysPut(ctx, firstIndex, keys: Uint8Array, fmt: 48 | 96)
+ *   keygen(ctx, sks: Uint8Array, cacheFirst: number) -> Uint8Array (48-B pubkeys)
+ *   sign(ctx, sks: Uint8Array, msgs: Uint8Array) -> Uint8Array (96-B signatures)
+ *   verify(ctx, jobs: {sets: {pkIndices: Uint32Array | pkBytes: Uint8Array (n x 96),
+ *                             msg: Uint8Array, sig: Uint8Array}[], batchable: boolean}[],
+ *          mode: 0 | 1) -> Promise<Int32Array>   (1 valid, 0 invalid, -code error)
+ *   strerror(code) -> string
+ *   close(ctx)
+ */
+#include <node_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/blsgpu.h"
+
+#define CHECK(env, x)                                         \
+  do {                                                        \
+    if ((x) != napi_ok) {                                     \
+      napi_throw_error((env), NULL, "blsgpu: N-API failure"); \
+      return NULL;                                            \
+    }                                                         \
+  } while (0)
+
+static napi_value throw_code(napi_env env, int rc) {
+  napi_throw_error(env, NULL, bgv_strerror(rc));
+  return NULL;
+}
+
+static bgv_ctx* get_ctx(napi_env env, napi_value v) {
+  void* p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+  return (bgv_ctx*)p;
+}
+
+static int get_bytes(napi_env env, napi_value v, uint8_t** data, size_t* len) {
+  napi_typedarray_type t;
+  size_t n, off;
+  void* d;
+  napi_value ab;
+  if (napi_get_typedarray_info(env, v, &t, &n, &d, &ab, &off) != napi_ok) return -1;
+  if (t == napi_uint8_array) {
+    *data = (uint8_t*)d;
+    *len = n;
+    return 0;
+  }
+  if (t == napi_uint32_array) {
+    *data = (uint8_t*)d;
+    *len = n * 4;
+    return 0;
+  }
+  return -1;
+}
+
+static napi_value js_init(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int devs[64];
+  int ndev = 0;
+  if (argc >= 1) {
+    bool is_arr = false;
+    napi_is_array(env, argv[0], &is_arr);
+    if (is_arr) {
+      uint32_t n = 0;
+      napi_get_array_length(env, argv[0], &n);
+      for (uint32_t i = 0; i < n && i < 64; ++i) {
+        napi_value e;
+        napi_get_element(env, argv[0], i, &e);
+        napi_get_value_int32(env, e, &devs[ndev++]);
+      }
+    }
+  }
+  bgv_ctx* ctx = NULL;
+  int rc = bgv_init(ndev ? devs : NULL, ndev, &ctx);
+  if (rc) return throw_code(env, rc);
+  napi_value out;
+  CHECK(env, napi_create_external(env, ctx, NULL, NULL, &out));
+  return out;
+}
+
+static napi_value js_close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  if (ctx) bgv_destroy(ctx);
+  return NULL;
+}
+
+static napi_value js_strerror(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  int32_t code = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  napi_get_value_int32(env, argv[0], &code);
+  CHECK(env, napi_create_string_utf8(env, bgv_strerror(code), NAPI_AUTO_LENGTH, &out));
+  return out;
+}
+
+static napi_value js_pubkeys_put(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint32_t first = 0;
+  int32_t fmt = 48;
+  uint8_t* keys;
+  size_t len;
+  napi_get_value_uint32(env, argv[1], &first);
+  if (get_bytes(env, argv[2], &keys, &len)) return throw_code(env, -BGV_E_ARG);
+  napi_get_value_int32(env, argv[3], &fmt);
+  int rc = bgv_pubkeys_put(ctx, first, keys, len / (size_t)fmt, fmt);
+  if (rc) return throw_code(env, rc);
+  return NULL;
+}
+
+static napi_value js_keygen(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], ab, out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t* sks;
+  size_t len;
+  int64_t first = -1;
+  if (get_bytes(env, argv[1], &sks, &len)) return throw_code(env, -BGV_E_ARG);
+  napi_get_value_int64(env, argv[2], &first);
+  void* dst;
+  CHECK(env, napi_create_arraybuffer(env, 48 * (len / 32), &dst, &ab));
+  int rc = bgv_keygen(ctx, sks, len / 32, first, (uint8_t*)dst);
+  if (rc) return throw_code(env, rc);
+  CHECK(env, napi_create_typedarray(env, napi_uint8_array, 48 * (len / 32), ab, 0, &out));
+  return out;
+}
+
+static napi_value js_sign(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], ab, out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t *sks, *msgs;
+  size_t l1, l2;
+  if (get_bytes(env, argv[1], &sks, &l1) || get_bytes(env, argv[2], &msgs, &l2) || l1 != l2)
+    return throw_code(env, -BGV_E_ARG);
+  void* dst;
+  CHECK(env, napi_create_arraybuffer(env, 96 * (l1 / 32), &dst, &ab));
+  int rc = bgv_sign(ctx, sks, msgs, l1 / 32, (uint8_t*)dst);
+  if (rc) return throw_code(env, rc);
+  CHECK(env, napi_create_typedarray(env, napi_uint8_array, 96 * (l1 / 32), ab, 0, &out));
+  return out;
+}
+
+/* ---- verify: napi_async_work + Promise ---------------------------------- */
+typedef struct {
+  bgv_ctx* ctx;
+  bgv_job* jobs;
+  size_t njobs;
+  bgv_set* sets;
+  size_t nsets;
+  int mode;
+  int32_t* codes;
+  int rc;
+  napi_deferred deferred;
+  napi_async_work work;
+  napi_ref* refs; /* keep every input buffer alive until completion */
+  size_t nrefs;
+} verify_req;
+
+static void verify_execute(napi_env env, void* data) {
+  (void)env;
+  verify_req* r = (verify_req*)data;
+  r->rc = bgv_verify(r->ctx, r->jobs, r->njobs, r->sets, r->nsets, r->mode, r->codes, NULL);
+}
+
+static void verify_complete(napi_env env, napi_status status, void* data) {
+  verify_req* r = (verify_req*)data;
+  if (status != napi_ok || r->rc) {
+    napi_value err, msg;
+    napi_create_string_utf8(env, bgv_strerror(r->rc ? r->rc : -BGV_E_DEVICE), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, r->deferred, err);
+  } else {
+    napi_value ab, arr;
+    void* dst;
+    napi_create_arraybuffer(env, 4 * r->njobs, &dst, &ab);
+    memcpy(dst, r->codes, 4 * r->njobs);
+    napi_create_typedarray(env, napi_int32_array, r->njobs, ab, 0, &arr);
+    napi_resolve_deferred(env, r->deferred, arr);
+  }
+  for (size_t i = 0; i < r->nrefs; ++i) napi_delete_reference(env, r->refs[i]);
+  napi_delete_async_work(env, r->work);
+  free(r->refs);
+  free(r->jobs);
+  free(r->sets);
+  free(r->codes);
+  free(r);
+}
+
+static napi_value js_verify(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  verify_req* r = (verify_req*)calloc(1, sizeof(verify_req));
+  r->ctx = get_ctx(env, argv[0]);
+  int32_t mode = 0;
+  if (argc >= 3) napi_get_value_int32(env, argv[2], &mode);
+  r->mode = mode;
+  uint32_t njobs = 0;
+  napi_get_array_length(env, argv[1], &njobs);
+  r->njobs = njobs;
+  r->jobs = (bgv_job*)calloc(njobs ? njobs : 1, sizeof(bgv_job));
+  r->codes = (int32_t*)calloc(njobs ? njobs : 1, sizeof(int32_t));
+  size_t cap = 64;
+  r->sets = (bgv_set*)calloc(cap, sizeof(bgv_set));
+  size_t refcap = 256;
+  r->refs = (napi_ref*)calloc(refcap, sizeof(napi_ref));
+  for (uint32_t j = 0; j < njobs; ++j) {
+    napi_value job, sets, bval;
+    napi_get_element(env, argv[1], j, &job);
+    napi_get_named_property(env, job, "sets", &sets);
+    napi_get_named_property(env, job, "batchable", &bval);
+    bool batchable = false;
+    napi_get_value_bool(env, bval, &batchable);
+    uint32_t ns = 0;
+    napi_get_array_length(env, sets, &ns);
+    r->jobs[j].first_set = (uint32_t)r->nsets;
+    r->jobs[j].n_sets = ns;
+    r->jobs[j].batchable = batchable;
+    for (uint32_t k = 0; k < ns; ++k) {
+      if (r->nsets == cap) {
+        cap *= 2;
+        r->sets = (bgv_set*)realloc(r->sets, cap * sizeof(bgv_set));
+      }
+      if (r->nrefs + 4 > refcap) {
+        refcap *= 2;
+        r->refs = (napi_ref*)realloc(r->refs, refcap * sizeof(napi_ref));
+      }
+      napi_value s, pk, msg, sig;
+      napi_get_element(env, sets, k, &s);
+      /* pkIndices (validator indices into the device cache) or pkBytes (n x 96-B uncompressed) */
+      bool by_index = false;
+      napi_has_named_property(env, s, "pkIndices", &by_index);
+      napi_get_named_property(env, s, by_index ? "pkIndices" : "pkBytes", &pk);
+      napi_get_named_property(env, s, "msg", &msg);
+      napi_get_named_property(env, s, "sig", &sig);
+      bgv_set* st = &r->sets[r->nsets++];
+      memset(st, 0, sizeof(*st));
+      uint8_t *pkd, *md, *sd;
+      size_t pkl, ml, sl;
+      if (get_bytes(env, pk, &pkd, &pkl) || get_bytes(env, msg, &md, &ml) || get_bytes(env, sig, &sd, &sl) ||
+          ml != 32 || (!by_index && pkl % 96)) {
+        for (size_t i = 0; i < r->nrefs; ++i) napi_delete_reference(env, r->refs[i]);
+        free(r->refs);
+        free(r->jobs);
+        free(r->sets);
+        free(r->codes);
+        free(r);
+        return throw_code(env, -BGV_E_ARG);
+      }
+      if (by_index) {
+        st->n_pk = (uint32_t)(pkl / 4);
+        st->pk_indices = (const uint32_t*)pkd;
+      } else {
+        st->n_pk = (uint32_t)(pkl / 96);
+        st->pk_bytes = pkd;
+      }
+      st->msg = md;
+      st->sig = sd;
+      st->sig_len = (uint32_t)sl;
+      napi_create_reference(env, pk, 1, &r->refs[r->nrefs++]);
+      napi_create_reference(env, msg, 1, &r->refs[r->nrefs++]);
+      napi_create_reference(env, sig, 1, &r->refs[r->nrefs++]);
+    }
+  }
+  napi_value promise, name;
+  CHECK(env, napi_create_promise(env, &r->deferred, &promise));
+  CHECK(env, napi_create_string_utf8(env, "blsgpu.verify", NAPI_AUTO_LENGTH, &name));
+  CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, r, &r->work));
+  CHECK(env, napi_queue_async_work(env, r->work));
+  return promise;
+}
+
+#define METHOD_ATTR ((napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable))
+
+static napi_value init_module(napi_env env, napi_value exports) {
+  napi_property_descriptor d[] = {
+      {"init", NULL, js_init, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"close", NULL, js_close, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"strerror", NULL, js_strerror, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"pubkeysPut", NULL, js_pubkeys_put, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"keygen", NULL, js_keygen, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"sign", NULL, js_sign, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"verify", NULL, js_verify, NULL, NULL, NULL, METHOD_ATTR, NULL},
+  };
+  napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
+  napi_value n;
+  napi_create_int32(env, bgv_device_count(), &n);
+  napi_set_named_property(env, exports, "deviceCount", n);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init_module)

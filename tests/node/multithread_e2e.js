@@ -1,0 +1,138 @@
+"use strict";
+// Node-side e2e of BlsGpuVerifier, the cases of the reference's
+// beacon-node/test/e2e/chain/bls/multithread.test.ts:22-118 run against the MI355X library.
+// Usage: node tests/node/multithread_e2e.js [cpu]   (cpu: load/export checks only, no device)
+const assert = require("assert");
+const path = require("path");
+const {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, addon} = require(
+  path.join(__dirname, "..", "..", "lodestar_amd", "node", "BlsGpuVerifier.js")
+);
+
+function cpuChecks() {
+  for (const f of ["init", "close", "strerror", "pubkeysPut", "keygen", "sign", "verify"]) {
+    assert.strictEqual(typeof addon[f], "function", f);
+  }
+  assert.strictEqual(addon.strerror(8), "BLST_INVALID_SIZE");
+  assert.strictEqual(addon.strerror(32), "QUEUE_ABORTED");
+  // multithread/utils.test.ts cases of chunkifyMaximizeChunkSize
+  const arr = (n) => Array.from({length: n}, (_, i) => i);
+  const shape = (n, m) => chunkifyMaximizeChunkSize(arr(n), m).map((c) => c.length);
+  assert.deepStrictEqual(shape(0, 128), [0]);
+  assert.deepStrictEqual(shape(1, 128), [1]);
+  assert.deepStrictEqual(shape(256, 128), [128, 128]);
+  assert.deepStrictEqual(shape(257, 128), [129, 128]);
+  assert.deepStrictEqual(shape(10, 3), [4, 4, 2]);
+  return {cpu: "ok", deviceCount: addon.deviceCount};
+}
+
+async function gpuChecks() {
+  const N = 3;
+  const sks = new Uint8Array(32 * N);
+  const msgs = new Uint8Array(32 * N);
+  for (let i = 0; i < N; i++) {
+    sks.fill(i + 1, 32 * i, 32 * (i + 1)); // SecretKey.fromBytes(Buffer.alloc(32, i + 1))
+    msgs.fill(i + 1, 32 * i, 32 * (i + 1));
+  }
+  const newPool = () => {
+    const pool = new BlsGpuVerifier({maxBufferWaitMs: 20});
+    addon.keygen(pool.ctx, sks, 0); // pubkeys cached at validator indices 0..N-1
+    return pool;
+  };
+  let pool = newPool();
+  const sigs = addon.sign(pool.ctx, sks, msgs);
+  const sets = [];
+  for (let i = 0; i < N; i++) {
+    sets.push({
+      type: SignatureSetType.single,
+      pubkey: i,
+      signingRoot: msgs.slice(32 * i, 32 * (i + 1)),
+      signature: sigs.slice(96 * i, 96 * (i + 1)),
+    });
+  }
+  const report = {};
+  async function many(sleep, opts) {
+    const ps = [];
+    for (let i = 0; i < 8; i++) {
+      ps.push(pool.verifySignatureSets(sets, opts));
+      if (sleep) await new Promise((r) => setTimeout(r, 5));
+    }
+    const res = await Promise.all(ps);
+    res.forEach((v, i) => assert.strictEqual(v, true, `sig set ${i} returned invalid`));
+  }
+  await many(false, undefined);
+  report.sync = "ok";
+  await many(true, undefined);
+  report.async = "ok";
+  await many(true, {batchable: true});
+  report.batched = "ok";
+
+  // batched, first is invalid: only its own promise rejects (multithread.test.ts:94-117)
+  const invalidSet = Object.assign({}, sets[0], {signature: new Uint8Array(32)});
+  const bad = pool.verifySignatureSets([invalidSet], {batchable: true});
+  const good = [];
+  for (let i = 0; i < 8; i++) good.push(pool.verifySignatureSets(sets, {batchable: true}));
+  await assert.rejects(bad, /BLST_INVALID_SIZE/);
+  (await Promise.all(good)).forEach((v) => assert.strictEqual(v, true));
+  report.firstInvalid = "ok";
+
+  // a wrong signature is false, not an error; mixed batch retried per job
+  const wrong = Object.assign({}, sets[0], {signature: sets[1].signature});
+  const w = pool.verifySignatureSets([wrong], {batchable: true});
+  const g2 = pool.verifySignatureSets(sets, {batchable: true});
+  assert.strictEqual(await w, false);
+  assert.strictEqual(await g2, true);
+  report.wrongSig = "ok";
+
+  // aggregate set: N signers of one message; the aggregate signature is the signature of
+  // sum(sk) mod r, the pubkey aggregate is summed from the device cache
+  const R = BigInt("0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001");
+  let skSum = 0n;
+  for (let i = 0; i < N; i++) skSum += BigInt("0x" + Buffer.from(sks.slice(32 * i, 32 * (i + 1))).toString("hex"));
+  const skAgg = Uint8Array.from(Buffer.from((skSum % R).toString(16).padStart(64, "0"), "hex"));
+  const root = new Uint8Array(32).fill(7);
+  const aggSig = addon.sign(pool.ctx, skAgg, root);
+  const aggSet = {type: SignatureSetType.aggregate, pubkeys: [0, 1, 2], signingRoot: root, signature: aggSig};
+  assert.strictEqual(await pool.verifySignatureSets([aggSet, ...sets], {batchable: true}), true);
+  const aggWrong = Object.assign({}, aggSet, {pubkeys: [0, 1]});
+  assert.strictEqual(await pool.verifySignatureSets([aggWrong]), false);
+  await assert.rejects(pool.verifySignatureSets([Object.assign({}, aggSet, {pubkeys: []})]), /EMPTY_AGGREGATE/);
+  report.aggregate = "ok";
+  // verifyOnMainThread path and a large call chunked into 128-set jobs
+  assert.strictEqual(await pool.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  const big = [];
+  for (let i = 0; i < 300; i++) big.push(sets[i % N]);
+  assert.strictEqual(await pool.verifySignatureSets(big, {batchable: true}), true);
+  report.chunked = "ok";
+
+  // golden vectors (tests/golden, oracle-signed) with pubkeys passed as 96-B bytes, not indices
+  const gold = (f) => JSON.parse(require("fs").readFileSync(path.join(__dirname, "..", "golden", f)));
+  const keys = gold("keys.json");
+  const hex = (h) => Uint8Array.from(Buffer.from(h, "hex"));
+  const gsets = gold("signatures.json").cases.slice(0, 8).map((c) => ({
+    type: SignatureSetType.single,
+    pubkey: hex(keys.pk_uncompressed[c.key]),
+    signingRoot: hex(c.msg),
+    signature: hex(c.sig),
+  }));
+  assert.strictEqual(await pool.verifySignatureSets(gsets, {batchable: true}), true);
+  const gswap = [Object.assign({}, gsets[0], {signature: gsets[1].signature})];
+  assert.strictEqual(await pool.verifySignatureSets(gswap, {batchable: true}), false);
+  report.goldenBytes = "ok";
+
+  // close(): queued work rejects with QUEUE_ABORTED, later calls too (index.ts:176-197,239-241)
+  const pending = pool.verifySignatureSets(sets, {batchable: true});
+  await pool.close();
+  await assert.rejects(pending, (e) => e instanceof QueueError && e.type.code === "QUEUE_ABORTED");
+  await assert.rejects(pool.verifySignatureSets(sets), (e) => e instanceof QueueError);
+  report.close = "ok";
+  return report;
+}
+
+(async () => {
+  const cpu = cpuChecks();
+  const out = process.argv[2] === "cpu" ? cpu : Object.assign(cpu, await gpuChecks());
+  console.log(JSON.stringify(out));
+})().catch((e) => {
+  console.error(e);
+  process.exit(1);
+});

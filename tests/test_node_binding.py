@@ -1,0 +1,39 @@
+"""The N-API addon and the JS BlsGpuVerifier (lodestar_amd/node/), driven through Node.
+
+CPU: the addon loads against libblsgpu.so and exports the binding; chunkify matches
+chain/bls/multithread/utils.ts:4-19.  GPU: the cases of the reference's
+beacon-node/test/e2e/chain/bls/multithread.test.ts:22-118 on the device.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "tests", "node", "multithread_e2e.js")
+ADDON = os.path.join(ROOT, "lodestar_amd", "node", "blsgpu.node")
+
+pytestmark = pytest.mark.skipif(shutil.which("node") is None, reason="node not in image")
+
+
+def _run(args, timeout):
+    if not os.path.exists(ADDON):
+        from lodestar_amd import build
+        assert build.build_node(verbose=False), "Node headers missing"
+    p = subprocess.run(["node", SCRIPT] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout + p.stderr
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_addon_loads_and_exports():
+    out = _run(["cpu"], 60)
+    assert out["cpu"] == "ok"
+
+
+@pytest.mark.gpu
+def test_node_verifier_e2e():
+    out = _run([], 110)
+    for k in ("sync", "async", "batched", "firstInvalid", "wrongSig", "aggregate", "chunked", "goldenBytes", "close"):
+        assert out[k] == "ok", out
