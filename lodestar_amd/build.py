@@ -27,26 +27,27 @@ def up_to_date(lib=LIB):
     return os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(d) for d in deps())
 
 
-def build(force=False, verbose=True):
-    if not force and up_to_date():
-        return LIB
+def build(force=False, verbose=True, lib=LIB, defines=()):
+    """defines: extra -D flags (tuning variants built to another `lib` path)."""
+    if not force and up_to_date(lib):
+        return lib
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = os.path.join(CSRC, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-c", src, "-o", obj]
+               "-c", src, "-o", obj] + ["-D" + d for d in defines]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs + ["-lpthread"]
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 NODE_DIR = os.path.join(HERE, "node")
@@ -75,5 +76,10 @@ def build_node(force=False, verbose=True):
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:  # --variant NAME DEF1 [DEF2 ...]: lodestar_amd/libblsgpu_NAME.so
+        i = sys.argv.index("--variant")
+        name, defs = sys.argv[i + 1], sys.argv[i + 2:]
+        print(build(force=True, lib=os.path.join(HERE, "libblsgpu_%s.so" % name), defines=defs))
+        sys.exit(0)
     build(force="--force" in sys.argv)
     build_node(force="--force" in sys.argv)

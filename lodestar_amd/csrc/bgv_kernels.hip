@@ -20,6 +20,12 @@
 #include "bls_hash.h"
 #include "bls_pairing.h"
 
+// Waves per SIMD the verify kernels are register-budgeted for (1: up to 512 VGPRs).
+#ifndef BGV_WPE
+#define BGV_WPE 1
+#endif
+#define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
+
 extern "C" {
 
 __device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
@@ -104,7 +110,7 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
 
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
-__global__ void __launch_bounds__(64) k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+__global__ void BGV_KATTR k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                              g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status,
                                              g2_aff* __restrict__ h, const uint32_t* __restrict__ pk_idx,
                                              const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
@@ -120,7 +126,7 @@ __global__ void __launch_bounds__(64) k_prep(const bgv_dslot* __restrict__ slots
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status);
 }
 
-__global__ void __launch_bounds__(64) k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+__global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                                const g1_aff* __restrict__ rpk, const g2_aff* __restrict__ h,
                                                const int32_t* __restrict__ sig_status,
                                                const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f) {
@@ -135,7 +141,7 @@ __global__ void __launch_bounds__(64) k_miller(const bgv_dslot* __restrict__ slo
 }
 
 // One wavefront per device group: LDS tree of Fp12 products and G2 sums.
-__global__ void __launch_bounds__(64) k_reduce(const bgv_dgroup* __restrict__ groups, const fp12_t* __restrict__ f,
+__global__ void BGV_KATTR k_reduce(const bgv_dgroup* __restrict__ groups, const fp12_t* __restrict__ f,
                                                const g2_jac* __restrict__ rsig,
                                                const int32_t* __restrict__ sig_status,
                                                const int32_t* __restrict__ pk_status, fp12_t* __restrict__ fg,
@@ -171,7 +177,7 @@ __global__ void __launch_bounds__(64) k_reduce(const bgv_dgroup* __restrict__ gr
 // Group closing, split in two launches to keep each kernel's stack small:
 //   k_final_ml   f_g *= MillerLoop(-G1, sum r_i sig_i)
 //   k_final      final exponentiation of f_g, verdict = (result == 1)
-__global__ void __launch_bounds__(64) k_final_ml(uint32_t ngroups, fp12_t* __restrict__ fg,
+__global__ void BGV_KATTR k_final_ml(uint32_t ngroups, fp12_t* __restrict__ fg,
                                                  const g2_jac* __restrict__ sg) {
   const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= ngroups) return;
@@ -179,7 +185,7 @@ __global__ void __launch_bounds__(64) k_final_ml(uint32_t ngroups, fp12_t* __res
   if (jac_to_aff(&sa, sg[gi])) fg[gi] = fp12_mul(fg[gi], miller_loop(g1_neg_generator(), sa));
 }
 
-__global__ void __launch_bounds__(64) k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
+__global__ void BGV_KATTR k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
                                               int32_t* __restrict__ verdict) {
   const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= ngroups) return;
@@ -293,6 +299,7 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 // Host-side launchers (declared in bgv_launch.h; called from bgv_api.cpp)
 // ---------------------------------------------------------------------------
 #include "bgv_launch.h"
+
 
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 
