@@ -211,7 +211,7 @@ def main():
         slots_per_launch = sum(s.sets_verified for s in stats) / max(1, launches)
         achieved = per_set[dom] * MACS_PER_FP_MUL * slots_per_launch / (avg[dom] * 1e-3)
         # whole-pipeline VALU figure: every verify kernel's counted work over the step time
-        per_group = opc["k_final_ml[per group]"] + opc["k_final_exp[per group]"]
+        per_group = opc["k_final[per group]"] + 6 * opc["k_reduce[per tree step]"]
         groups = statistics.mean(s.device_groups for s in stats)
         pipeline_macs = (sum(per_set.values()) * slots + per_group * groups) * MACS_PER_FP_MUL * args.steps * world
         pipeline_frac = pipeline_macs / elapsed / (PEAK_MAC_PER_S * world)

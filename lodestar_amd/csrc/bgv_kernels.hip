@@ -1,18 +1,23 @@
 // Batch BLS12-381 signature-set verification kernels for CDNA4 (gfx950).
 //
-// One signature set per lane.  A verify call runs these kernels in order on
-// one HIP stream (see bgv_api.cpp):
+// One signature set per lane.  A verify call runs these kernels in order (see
+// bgv_api.cpp):
 //
-//   k_sig      decompress + subgroup-check the 96-byte signature, r_i * sig_i
-//   k_hash     hash_to_G2(signing root) -> affine H(m_i)
-//   k_pk       gather + aggregate pubkeys from the device cache, r_i * pk_i -> affine
-//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i))
-//   k_reduce   per device group (one wavefront): prod f_i and sum r_i sig_i via an LDS tree
-//   k_final    per group: f * MillerLoop(-G1, sum r_i sig_i) -> final exponentiation -> == 1
+//   k_prep     three independent tasks side by side (blockIdx.y):
+//              sig  decompress + subgroup-check the 96-byte signature -> affine sig_i
+//              hash hash_to_G2(signing root) -> affine H(m_i)
+//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i and
+//                   r_i * (-G1), both made affine with one shared inversion
+//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)) * MillerLoop(-r_i G1, sig_i), one
+//              shared Fp12 accumulator (2-pair loop)
+//   k_reduce   per device group (one wavefront): prod f_i via an LDS tree
+//   k_final    per group: final exponentiation -> == 1
 //
 // This is the randomized batch equation of blst's verifyMultipleAggregateSignatures
 // (called from packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25):
-//   prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i) == 1.
+//   prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i) == 1,
+// with e(-G1, sum r_i sig_i) = prod_i e(-r_i G1, sig_i) moved into the per-set
+// kernel, so a group closes with a product and one final exponentiation only.
 // A one-set group is the core verify of maybeBatch.ts:34-38 raised to the
 // power r (nonzero, < group order), which has the same verdict.
 #include "bgv_layout.h"
@@ -24,15 +29,20 @@
 #ifndef BGV_WPE
 #define BGV_WPE 1
 #endif
+// k_prep runs 3 x nslots lanes of shorter tasks: two waves per SIMD measured faster
+// (36.6 vs 45.3 ms per 131072 slots), the long-chain kernels stay at one.
+#ifndef BGV_WPE_PREP
+#define BGV_WPE_PREP 2
+#endif
 #define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
+#define BGV_KATTR_PREP __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_PREP, BGV_WPE_PREP)))
 
 extern "C" {
 
-__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
+__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* __restrict__ sig,
                                       int32_t* __restrict__ sig_status) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
-  g2_jac out = jac_infinity<fp2_t>();
   if (d.flags & BGV_SLOT_PAD) {
     st = BGV_ST_INFINITY;
   } else if (d.sig_len != 96) {
@@ -44,18 +54,14 @@ __device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ 
     bool inf;
     st = g2_decompress(&a, &inf, b);
     if (st == BGV_OK) {
-      if (inf) {
+      if (inf)
         st = BGV_ST_INFINITY;  // skipped in the accumulator, as blst does
-      } else {
-        const g2_jac j = jac_from_aff(a);
-        if (!g2_in_subgroup(j))
-          st = BGV_POINT_NOT_IN_GROUP;
-        else
-          out = jac_mul_u64(j, d.scalar);
-      }
+      else if (!g2_in_subgroup(jac_from_aff(a)))
+        st = BGV_POINT_NOT_IN_GROUP;
+      else
+        sig[s] = a;
     }
   }
-  rsig[s] = out;
   sig_status[s] = st;
 }
 
@@ -72,7 +78,7 @@ __device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__
 __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                     int32_t* __restrict__ pk_status) {
+                                     g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
   if (d.flags & BGV_SLOT_PAD) {
@@ -99,102 +105,82 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
     acc = jac_add_aff(acc, a);
   }
   if (st == BGV_OK) {
-    g1_aff out;
-    if (jac_to_aff(&out, jac_mul_u64(acc, d.scalar)))
-      rpk[s] = out;
-    else
+    const g1_jac a = jac_mul_u64(acc, d.scalar);
+    if (jac_is_inf(a)) {
       st = BGV_ST_INFINITY;
+    } else {
+      // r_i * (-G1) for the signature's pair; never infinity (0 < r_i < group order)
+      const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), d.scalar);
+      g1_aff pa, ga;
+      jac2_to_aff(&pa, &ga, a, g);
+      rpk[s] = pa;
+      rg[s] = ga;
+    }
   }
   pk_status[s] = st;
 }
 
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
-__global__ void BGV_KATTR k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                             g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status,
-                                             g2_aff* __restrict__ h, const uint32_t* __restrict__ pk_idx,
-                                             const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
-                                             g1_aff* __restrict__ rpk, int32_t* __restrict__ pk_status) {
+__global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_aff* __restrict__ sig,
+                                 int32_t* __restrict__ sig_status, g2_aff* __restrict__ h,
+                                 const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                 const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                 g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   // hash first: the longest task starts earliest
   if (blockIdx.y == 0)
     task_hash(s, slots, h);
   else if (blockIdx.y == 1)
-    task_sig(s, slots, rsig, sig_status);
+    task_sig(s, slots, sig, sig_status);
   else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status);
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status);
 }
 
+// f_i = MillerLoop(r pk, H(m)) * MillerLoop(-r G1, sig); 1 for slots that do not
+// take part (padding, failed decode/aggregation).  An infinity signature keeps
+// its pubkey pair and drops the signature pair, as blst's accumulator does.
 __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                               const g1_aff* __restrict__ rpk, const g2_aff* __restrict__ h,
-                                               const int32_t* __restrict__ sig_status,
-                                               const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f) {
+                                   const g1_aff* __restrict__ rpk, const g2_aff* __restrict__ h,
+                                   const g1_aff* __restrict__ rg, const g2_aff* __restrict__ sig,
+                                   const int32_t* __restrict__ sig_status, const int32_t* __restrict__ pk_status,
+                                   fp12_t* __restrict__ f) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   const int32_t ss = sig_status[s];
   const bool live = !(slots[s].flags & BGV_SLOT_PAD) && (ss == BGV_ST_OK || ss == BGV_ST_INFINITY) &&
                     pk_status[s] == BGV_ST_OK;
   fp12_t r = fp12_one();
-  if (live) r = miller_loop(rpk[s], h[s]);
+  if (live) r = miller_loop2(rpk[s], h[s], rg[s], sig[s], ss == BGV_ST_OK);
   f[s] = r;
 }
 
-// One wavefront per device group: LDS tree of Fp12 products and G2 sums.
+// One wavefront per device group: LDS tree of Fp12 products.
 __global__ void BGV_KATTR k_reduce(const bgv_dgroup* __restrict__ groups, const fp12_t* __restrict__ f,
-                                               const g2_jac* __restrict__ rsig,
-                                               const int32_t* __restrict__ sig_status,
-                                               const int32_t* __restrict__ pk_status, fp12_t* __restrict__ fg,
-                                               g2_jac* __restrict__ sg) {
+                                   fp12_t* __restrict__ fg) {
   extern __shared__ uint32_t lds[];
   fp12_t* lf = reinterpret_cast<fp12_t*>(lds);
-  g2_jac* ls = reinterpret_cast<g2_jac*>(lds + BGV_WAVE * (sizeof(fp12_t) / 4));
   const bgv_dgroup g = groups[blockIdx.x];
   const uint32_t j = threadIdx.x;
   fp12_t mf = fp12_one();
-  g2_jac ms = jac_infinity<fp2_t>();
-  if (j < g.n_slots) {
-    const uint32_t s = g.first_slot + j;
-    mf = f[s];
-    if (sig_status[s] == BGV_ST_OK && pk_status[s] == BGV_ST_OK) ms = rsig[s];
-  }
+  if (j < g.n_slots) mf = f[g.first_slot + j];
   for (uint32_t d = 1; d < BGV_WAVE; d <<= 1) {
     lf[j] = mf;
-    ls[j] = ms;
     __syncthreads();
-    if ((j & (2 * d - 1)) == 0 && j + d < g.n_slots) {
-      mf = fp12_mul(mf, lf[j + d]);
-      ms = jac_add(ms, ls[j + d]);
-    }
+    if ((j & (2 * d - 1)) == 0 && j + d < g.n_slots) mf = fp12_mul(mf, lf[j + d]);
     __syncthreads();
   }
-  if (j == 0) {
-    fg[blockIdx.x] = mf;
-    sg[blockIdx.x] = ms;
-  }
+  if (j == 0) fg[blockIdx.x] = mf;
 }
 
-// Group closing, split in two launches to keep each kernel's stack small:
-//   k_final_ml   f_g *= MillerLoop(-G1, sum r_i sig_i)
-//   k_final      final exponentiation of f_g, verdict = (result == 1)
-__global__ void BGV_KATTR k_final_ml(uint32_t ngroups, fp12_t* __restrict__ fg,
-                                                 const g2_jac* __restrict__ sg) {
-  const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= ngroups) return;
-  g2_aff sa;
-  if (jac_to_aff(&sa, sg[gi])) fg[gi] = fp12_mul(fg[gi], miller_loop(g1_neg_generator(), sa));
-}
-
-__global__ void BGV_KATTR k_final(uint32_t ngroups, const fp12_t* __restrict__ fg,
-                                              int32_t* __restrict__ verdict) {
+// Group closing: final exponentiation of the group product, verdict = (result == 1).
+__global__ void BGV_KATTR k_final(uint32_t ngroups, const fp12_t* __restrict__ fg, int32_t* __restrict__ verdict) {
   const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
   if (gi >= ngroups) return;
   verdict[gi] = fp12_is_one(final_exp(fg[gi])) ? 1 : 0;
 }
 
-// ---------------------------------------------------------------------------
-// Parity hooks (bgv_aggregate_pubkeys / bgv_hash_to_g2 in the C-ABI)
-// ---------------------------------------------------------------------------
 __global__ void k_aggregate_cached(const uint32_t* __restrict__ idx, uint32_t n, const g1_aff* __restrict__ cache,
                                    uint8_t* __restrict__ out96) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -311,12 +297,13 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
   BGV_MARK(0);
-  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
-                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status);
+  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.sig, b.sig_status, b.h,
+                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.rg,
+                     b.pk_status);
   BGV_MARK(1);
   BGV_MARK(2);
-  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
-                     b.pk_status, b.f);
+  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.rg, b.sig,
+                     b.sig_status, b.pk_status, b.f);
   BGV_MARK(3);
   return hipGetLastError();
 }
@@ -325,34 +312,32 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
 // the first pass and, over the same per-slot results, for the per-job retry pass.
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
   if (b.ngroups == 0) return hipSuccess;
-  const size_t lds = BGV_WAVE * (sizeof(fp12_t) + sizeof(g2_jac));
+  const size_t lds = BGV_WAVE * sizeof(fp12_t);
   BGV_MARK(4);
-  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.rsig, b.sig_status,
-                     b.pk_status, b.fg, b.sg);
+  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.fg);
   BGV_MARK(5);
   BGV_MARK(6);
-  hipLaunchKernelGGL(k_final_ml, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.sg);
-  BGV_MARK(7);
-  BGV_MARK(8);
   hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.verdict);
-  BGV_MARK(9);
+  BGV_MARK(7);
   return hipGetLastError();
 }
 #undef BGV_MARK
 
 size_t bgv_slot_bytes() {
-  return sizeof(g2_jac) + sizeof(g2_aff) + sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
+  return 2 * sizeof(g2_aff) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
 }
-size_t bgv_group_bytes() { return sizeof(fp12_t) + sizeof(g2_jac) + sizeof(int32_t); }
+size_t bgv_group_bytes() { return sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
 
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
   uint8_t* p = static_cast<uint8_t*>(slot_mem);
-  b->rsig = reinterpret_cast<g2_jac*>(p);
-  p += sizeof(g2_jac) * (size_t)cap_slots;
+  b->sig = reinterpret_cast<g2_aff*>(p);
+  p += sizeof(g2_aff) * (size_t)cap_slots;
   b->h = reinterpret_cast<g2_aff*>(p);
   p += sizeof(g2_aff) * (size_t)cap_slots;
   b->rpk = reinterpret_cast<g1_aff*>(p);
+  p += sizeof(g1_aff) * (size_t)cap_slots;
+  b->rg = reinterpret_cast<g1_aff*>(p);
   p += sizeof(g1_aff) * (size_t)cap_slots;
   b->f = reinterpret_cast<fp12_t*>(p);
   p += sizeof(fp12_t) * (size_t)cap_slots;
@@ -362,8 +347,6 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   uint8_t* q = static_cast<uint8_t*>(group_mem);
   b->fg = reinterpret_cast<fp12_t*>(q);
   q += sizeof(fp12_t) * (size_t)cap_groups;
-  b->sg = reinterpret_cast<g2_jac*>(q);
-  q += sizeof(g2_jac) * (size_t)cap_groups;
   b->verdict = reinterpret_cast<int32_t*>(q);
 }
 

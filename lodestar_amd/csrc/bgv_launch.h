@@ -26,14 +26,14 @@ struct bgv_dev_batch {
   const bgv_cache_entry* cache_opaque;
   const uint8_t* pk_bytes;
   // carved per-slot / per-group scratch
-  jac_t<fp2_t>* rsig;
-  aff_t<fp2_t>* h;
-  aff_t<fp_t>* rpk;
-  fp12_t* f;
+  aff_t<fp2_t>* sig;  // decompressed signatures
+  aff_t<fp2_t>* h;    // H(m_i)
+  aff_t<fp_t>* rpk;   // r_i * aggregated pubkey
+  aff_t<fp_t>* rg;    // r_i * (-G1)
+  fp12_t* f;          // per-slot 2-pair Miller loop value
   int32_t* sig_status;
   int32_t* pk_status;
-  fp12_t* fg;
-  jac_t<fp2_t>* sg;
+  fp12_t* fg;  // per-group product
   int32_t* verdict;
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
@@ -41,9 +41,9 @@ struct bgv_dev_batch {
 };
 
 // kernels of one verify launch, in order (names for per-kernel timing)
-#define BGV_NKERNELS 5
+#define BGV_NKERNELS 4
 #define BGV_NSETKERNELS 2  // the first BGV_NSETKERNELS run once per call (bgv_launch_sets)
-static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_prep", "k_miller", "k_reduce", "k_final_ml", "k_final"};
+static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_prep", "k_miller", "k_reduce", "k_final"};
 struct bgv_streams {
   hipStream_t main;
   hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr

@@ -176,6 +176,19 @@ BGV_NOINLINE bool jac_to_aff(aff_t<F>* out, const jac_t<F>& p) {
   return !jac_is_inf(p);
 }
 
+// Two finite Jacobian points -> affine with one shared inversion.
+template <class F>
+BGV_NOINLINE void jac2_to_aff(aff_t<F>* a, aff_t<F>* b, const jac_t<F>& p, const jac_t<F>& q) {
+  const F zi = f_inv(f_mul(p.z, q.z));
+  const F pzi = f_mul(zi, q.z), qzi = f_mul(zi, p.z);
+  F t = f_sqr(pzi);
+  a->x = f_mul(p.x, t);
+  a->y = f_mul(p.y, f_mul(t, pzi));
+  t = f_sqr(qzi);
+  b->x = f_mul(q.x, t);
+  b->y = f_mul(q.y, f_mul(t, qzi));
+}
+
 template <class F>
 BGV_HD bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);

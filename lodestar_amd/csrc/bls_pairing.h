@@ -76,6 +76,39 @@ BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
   return fp12_conj(f);
 }
 
+// f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) (conjugated) with one shared accumulator: the
+// squarings of f are paid once for both pairs.  two == false drops the second pair.
+BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_aff& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
+  const fp_t xn1 = fp_neg(p1.x), xn2 = fp_neg(p2.x);
+  g2_jac t1 = jac_from_aff(q1), t2 = jac_from_aff(q2);
+  fp2_t l0, l1, l3;
+  const uint64_t X = BGV_X_ABS;
+  miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
+  fp12_t f = fp12_mul_line(fp12_one(), l0, l1, l3);
+  if (two) {
+    miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
+    f = fp12_mul_line(f, l0, l1, l3);
+  }
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if ((X >> (i + 1)) & 1) {
+      miller_add(t1, &l0, &l1, &l3, q1, xn1, p1.y);
+      f = fp12_mul_line(f, l0, l1, l3);
+      if (two) {
+        miller_add(t2, &l0, &l1, &l3, q2, xn2, p2.y);
+        f = fp12_mul_line(f, l0, l1, l3);
+      }
+    }
+    f = fp12_sqr(f);
+    miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
+    f = fp12_mul_line(f, l0, l1, l3);
+    if (two) {
+      miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
+      f = fp12_mul_line(f, l0, l1, l3);
+    }
+  }
+  return fp12_conj(f);
+}
+
 // a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
 BGV_NOINLINE fp12_t cyclotomic_pow_x(const fp12_t& a) {
   const uint64_t X = BGV_X_ABS;

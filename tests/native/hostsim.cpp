@@ -45,14 +45,11 @@ void hs_count_reset() { bgv_count_mul = bgv_count_sqr = 0; }
 unsigned long long hs_count_mul() { return bgv_count_mul; }
 unsigned long long hs_count_sqr() { return bgv_count_sqr; }
 // per-lane bodies of the verify kernels (bgv_kernels.hip), for counting only
-int hs_k_sig_body(const uint8_t* sig96, uint64_t r) {
+int hs_k_sig_body(const uint8_t* sig96) {
   g2_aff a;
   bool inf;
   if (g2_decompress(&a, &inf, sig96) || inf) return 0;
-  const g2_jac j = jac_from_aff(a);
-  if (!g2_in_subgroup(j)) return 0;
-  g2_jac o = jac_mul_u64(j, r);
-  return !jac_is_inf(o);
+  return g2_in_subgroup(jac_from_aff(a));
 }
 int hs_k_hash_body(const uint8_t* msg32) {
   g2_aff a;
@@ -62,24 +59,17 @@ int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_aff p = in_g1(pk_aff_tl);
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
-  g1_aff o;
-  return jac_to_aff(&o, jac_mul_u64(acc, r));
+  const g1_jac a = jac_mul_u64(acc, r);
+  const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), r);
+  g1_aff pa, ga;
+  jac2_to_aff(&pa, &ga, a, g);
+  return 1;
 }
-void hs_k_miller_body(const uint8_t* p, const uint8_t* q) { (void)miller_loop(in_g1(p), in_g2(q)); }
-void hs_k_final_body(const uint8_t* f, const uint8_t* s_aff) {
-  fp12_t x = fp12_mul(in_fp12(f), miller_loop(g1_neg_generator(), in_g2(s_aff)));
-  (void)fp12_is_one(final_exp(x));
+void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
+  (void)miller_loop2(in_g1(p), in_g2(q), g1_neg_generator(), in_g2(q), true);
 }
-void hs_k_final_ml_body(const uint8_t* f, const uint8_t* s_aff) {
-  g2_aff sa;
-  (void)jac_to_aff(&sa, jac_from_aff(in_g2(s_aff)));
-  (void)fp12_mul(in_fp12(f), miller_loop(g1_neg_generator(), sa));
-}
-void hs_k_final_exp_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
-void hs_k_reduce_step(const uint8_t* f, const uint8_t* s_aff) {
-  (void)fp12_mul(in_fp12(f), in_fp12(f));
-  (void)jac_add(jac_from_aff(in_g2(s_aff)), jac_dbl(jac_from_aff(in_g2(s_aff))));
-}
+void hs_k_final_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
+void hs_k_reduce_step(const uint8_t* f) { (void)fp12_mul(in_fp12(f), in_fp12(f)); }
 #endif
 
 void hs_fp_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_mul(in_fp(a), in_fp(b))); }
@@ -186,6 +176,19 @@ int hs_hash_to_g2(uint8_t* out_aff, uint8_t* out_comp96, const uint8_t* msg, uin
 // P (test layout g1) , Q (test layout g2) -> Miller loop value and pairing^3
 void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12(out, miller_loop(in_g1(p), in_g2(q))); }
 void hs_final_exp(uint8_t* out, const uint8_t* f) { out_fp12(out, final_exp(in_fp12(f))); }
+void hs_miller_loop2(uint8_t* out, const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2,
+                     int two) {
+  out_fp12(out, miller_loop2(in_g1(p1), in_g2(q1), in_g1(p2), in_g2(q2), two != 0));
+}
+// per-set path of k_prep's pk task + k_miller for one single set: r pk, r (-G1) via the
+// shared-inversion affine conversion, then the 2-pair loop and the final exponentiation
+int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* sig_aff, uint64_t r) {
+  const g1_jac a = jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r);
+  const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), r);
+  g1_aff pa, ga;
+  jac2_to_aff(&pa, &ga, a, g);
+  return fp12_is_one(final_exp(miller_loop2(pa, in_g2(h_aff), ga, in_g2(sig_aff), true)));
+}
 
 int hs_g1_decompress(uint8_t* out, const uint8_t* in48) {
   g1_aff a;

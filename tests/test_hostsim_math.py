@@ -250,3 +250,33 @@ def test_pairing(L):
     L.hs_final_exp(fe, ml.raw)
     want = o.f12_pow(o.pairing(p, q), 3)  # device final exp computes e(P,Q)^3
     assert hs.b_fp12_tower(fe.raw) == o.f12_to_tower_list(want)
+
+
+def test_miller_loop2(L):
+    """The per-set 2-pair loop equals the product of the two single loops, and the
+    second pair drops out when two == 0."""
+    p1 = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    p2 = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    q1, q2 = g2_rand_in_group(), g2_rand_in_group()
+    m1, m2, both, one = hs.buf(576), hs.buf(576), hs.buf(576), hs.buf(576)
+    L.hs_miller_loop(m1, hs.g1_b(p1), hs.g2_b(q1))
+    L.hs_miller_loop(m2, hs.g1_b(p2), hs.g2_b(q2))
+    L.hs_miller_loop2(both, hs.g1_b(p1), hs.g2_b(q1), hs.g1_b(p2), hs.g2_b(q2), 1)
+    L.hs_miller_loop2(one, hs.g1_b(p1), hs.g2_b(q1), hs.g1_b(p2), hs.g2_b(q2), 0)
+    prod = hs.buf(576)
+    L.hs_fp12_mul(prod, m1.raw, m2.raw)
+    assert both.raw == prod.raw
+    assert one.raw == m1.raw
+
+
+def test_verify_one_two_pair(L):
+    """k_prep pk task + k_miller + k_final for one set: e(r pk, H) e(-r G1, sig) == 1."""
+    sk = o.interop_secret_key(5)
+    pk = o.sk_to_pk(sk)
+    msg = bytes(range(32))
+    h = o.hash_to_g2(msg)
+    sig = o.sign(sk, msg)
+    r = rnd.getrandbits(64) | 1
+    assert L.hs_verify_one(hs.g1_b(pk), hs.g2_b(h), hs.g2_b(sig), r) == 1
+    other = o.sign(o.interop_secret_key(6), msg)
+    assert L.hs_verify_one(hs.g1_b(pk), hs.g2_b(h), hs.g2_b(other), r) == 0

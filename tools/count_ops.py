@@ -42,12 +42,7 @@ def main():
     sig = o.sign(sk, msg)
     out = {}
     trials = 8
-    acc = [0, 0]
-    for _ in range(trials):
-        m, s = count(lambda: L.hs_k_sig_body(o.g2_compress(sig), ctypes.c_uint64(rng.getrandbits(64) | 1)))
-        acc[0] += m
-        acc[1] += s
-    out["k_sig"] = [acc[0] / trials, acc[1] / trials]
+    out["k_sig"] = list(count(lambda: L.hs_k_sig_body(o.g2_compress(sig))))
     out["k_hash"] = list(count(lambda: L.hs_k_hash_body(msg)))
     for npk in (1, 128):
         acc = [0, 0]
@@ -59,10 +54,8 @@ def main():
     h = o.hash_to_g2(msg)
     out["k_miller"] = list(count(lambda: L.hs_k_miller_body(hs.g1_b(pk), hs.g2_b(h))))
     f12 = hs.fp12_b_tower([rng.randrange(o.P) for _ in range(12)])
-    out["k_final[per group]"] = list(count(lambda: L.hs_k_final_body(f12, hs.g2_b(sig))))
-    out["k_final_ml[per group]"] = list(count(lambda: L.hs_k_final_ml_body(f12, hs.g2_b(sig))))
-    out["k_final_exp[per group]"] = list(count(lambda: L.hs_k_final_exp_body(f12)))
-    out["k_reduce[per tree step]"] = list(count(lambda: L.hs_k_reduce_step(f12, hs.g2_b(sig))))
+    out["k_final[per group]"] = list(count(lambda: L.hs_k_final_body(f12)))
+    out["k_reduce[per tree step]"] = list(count(lambda: L.hs_k_reduce_step(f12)))
     res = {
         "note": "Fp products [mul, sqr] per set (per group / per tree step where named), counted in the "
                 "kernels' own math (host build, -DBGV_COUNT_OPS). Fp-mul-eq = mul + sqr; "
