@@ -37,8 +37,10 @@
 #include "../../include/blsgpu.h"
 #include "bgv_launch.h"
 
-// parts a failing mixed group is split into per retry round (BGV_RETRY_FANOUT env)
-#define BGV_RETRY_FANOUT 64
+// parts a failing mixed group is split into per retry round (BGV_RETRY_FANOUT env).
+// Group closings are team-parallel and cheap in latency, so bisecting (64 -> 8 -> 1)
+// costs an extra round but ~4x fewer final exponentiations than going per job at once.
+#define BGV_RETRY_FANOUT 8
 // slots merged into one device super-batch (BGV_MAX_BATCH_SLOTS env)
 #define BGV_MAX_BATCH_SLOTS 131072
 // dispatcher threads (= HIP streams) per device (BGV_DISPATCHERS env)
@@ -89,6 +91,31 @@ extern "C" int bgv_device_count(void) {
 
 namespace {
 
+// Page-locked host staging: copies from it run on the DMA engines, whereas pageable
+// copies are staged by blit kernels that queue behind the verify kernels on the CUs.
+template <class T>
+struct Pinned {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    release();
+    n = std::max(n, 2 * cap);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(n, 1) * sizeof(T), 0);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = n;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 // One dispatcher's device resources: its stream, events and buffers.
 struct Exec {
   hipStream_t main = nullptr;   // per-set kernels (compute-bound)
@@ -105,6 +132,12 @@ struct Exec {
   size_t idx_cap = 0;
   uint8_t* d_pkb = nullptr;
   size_t pkb_cap = 0;
+  // host staging of one super-batch
+  Pinned<bgv_dslot> h_slots;
+  Pinned<bgv_dgroup> h_groups;
+  Pinned<uint32_t> h_idx;
+  Pinned<uint8_t> h_pkb;
+  Pinned<int32_t> h_ss, h_ps, h_verdict;
 };
 
 struct Device {
@@ -336,6 +369,13 @@ static void exec_destroy(Exec* x) {
   void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  x->h_slots.release();
+  x->h_groups.release();
+  x->h_idx.release();
+  x->h_pkb.release();
+  x->h_ss.release();
+  x->h_ps.release();
+  x->h_verdict.release();
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
   if (x->ev_sets) (void)hipEventDestroy(x->ev_sets);
@@ -606,25 +646,37 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     nidx += call->L.idx.size();
     npkb += call->L.pkb.size();
   }
-  std::vector<bgv_dslot> slots;
-  slots.reserve(nslots);
-  std::vector<bgv_dgroup> groups;
-  groups.reserve(ngroups);
-  std::vector<uint32_t> idx;
-  idx.reserve(nidx);
-  std::vector<uint8_t> pkb;
-  pkb.reserve(npkb);
-  for (Call* call : calls) {
-    const uint32_t ib = (uint32_t)idx.size(), pb = (uint32_t)(pkb.size() / 96), gb = (uint32_t)groups.size();
-    for (bgv_dslot s : call->L.slots) {
-      if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
-      if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
-      if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
-      slots.push_back(s);
+  HIPCHK(hipSetDevice(d.id));
+  int rc;
+  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
+      (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1))) ||
+      (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
+    return rc;
+  HIPCHK(x.h_slots.reserve(nslots));
+  HIPCHK(x.h_groups.reserve(std::max<size_t>(ngroups, 1)));
+  HIPCHK(x.h_idx.reserve(nidx));
+  HIPCHK(x.h_pkb.reserve(npkb));
+  HIPCHK(x.h_ss.reserve(nslots));
+  HIPCHK(x.h_ps.reserve(nslots));
+  HIPCHK(x.h_verdict.reserve(std::max<size_t>(ngroups, 1)));
+  bgv_dslot* slots = x.h_slots.p;
+  bgv_dgroup* groups = x.h_groups.p;
+  {
+    size_t ns = 0, ng = 0, ni = 0, npb = 0;
+    for (Call* call : calls) {
+      const uint32_t ib = (uint32_t)ni, pb = (uint32_t)(npb / 96), gb = (uint32_t)ng;
+      for (bgv_dslot s : call->L.slots) {
+        if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
+        if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
+        if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
+        slots[ns++] = s;
+      }
+      for (bgv_dgroup g : call->L.groups) groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots};
+      if (!call->L.idx.empty()) memcpy(x.h_idx.p + ni, call->L.idx.data(), 4 * call->L.idx.size());
+      ni += call->L.idx.size();
+      if (!call->L.pkb.empty()) memcpy(x.h_pkb.p + npb, call->L.pkb.data(), call->L.pkb.size());
+      npb += call->L.pkb.size();
     }
-    for (bgv_dgroup g : call->L.groups) groups.push_back(bgv_dgroup{g.first_slot + call->slot_base, g.n_slots});
-    idx.insert(idx.end(), call->L.idx.begin(), call->L.idx.end());
-    pkb.insert(pkb.end(), call->L.pkb.begin(), call->L.pkb.end());
   }
   std::vector<uint64_t> sc(nslots);
   fill_scalars(c, sc.data(), nslots);
@@ -636,20 +688,14 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     prof = c->profile;
   }
   t_merge = ms_since(tb);
-  HIPCHK(hipSetDevice(d.id));
-  int rc;
-  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
-      (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1))) ||
-      (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
-    return rc;
-  HIPCHK(hipMemcpyAsync(x.d_slots, slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
-  HIPCHK(hipMemcpyAsync(x.d_groups, groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
-  if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, idx.data(), 4 * nidx, hipMemcpyHostToDevice, x.main));
-  if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, pkb.data(), npkb, hipMemcpyHostToDevice, x.main));
+  HIPCHK(hipMemcpyAsync(x.d_slots, slots, sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
+  HIPCHK(hipMemcpyAsync(x.d_groups, groups, sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
+  if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, x.h_idx.p, 4 * nidx, hipMemcpyHostToDevice, x.main));
+  if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, x.h_pkb.p, npkb, hipMemcpyHostToDevice, x.main));
   bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
   bgv_streams S{x.main, prof ? x.kev : nullptr};
   bgv_streams SC{x.close, prof ? x.kev : nullptr};
-  std::vector<int32_t> ss(nslots), ps(nslots), verdict(ngroups);
+  int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;
   {
     // One super-batch at a time runs the compute-bound per-set kernels; the
     // latency-bound group closing of one batch then overlaps the next batch's
@@ -666,9 +712,9 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   const auto tg = std::chrono::steady_clock::now();
   HIPCHK(bgv_launch_groups(b, SC));
   HIPCHK(hipEventRecord(x.ev1, x.close));
-  HIPCHK(hipMemcpyAsync(ss.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
-  HIPCHK(hipMemcpyAsync(ps.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
-  HIPCHK(hipMemcpyAsync(verdict.data(), b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
+  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.close));
   HIPCHK(hipStreamSynchronize(x.close));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
@@ -679,7 +725,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     uint32_t gb = 0;
     for (Call* call : calls) {
       call->st.device_ms += ms;
-      call_after_pass1(call, ss.data() + call->slot_base, ps.data() + call->slot_base, verdict.data() + gb);
+      call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb);
       gb += (uint32_t)call->L.groups.size();
     }
   }
@@ -698,13 +744,16 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     ++rounds;
     const uint32_t nrg = (uint32_t)rg.size();
     if ((rc = exec_reserve_groups(x, nrg))) return rc;
-    std::vector<int32_t> rv(nrg);
-    HIPCHK(hipMemcpyAsync(x.d_groups, rg.data(), sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
+    HIPCHK(x.h_groups.reserve(nrg));
+    HIPCHK(x.h_verdict.reserve(nrg));
+    memcpy(x.h_groups.p, rg.data(), sizeof(bgv_dgroup) * nrg);
+    int32_t* rv = x.h_verdict.p;
+    HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
     b = make_batch(d, x, nslots, nrg);
     HIPCHK(hipEventRecord(x.ev0, x.close));
     HIPCHK(bgv_launch_groups(b, SC));
     HIPCHK(hipEventRecord(x.ev1, x.close));
-    HIPCHK(hipMemcpyAsync(rv.data(), b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
+    HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
     HIPCHK(hipStreamSynchronize(x.close));
     HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
     if (prof) prof_add(c, x, false, true);
@@ -715,7 +764,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
       call->st.device_groups += mine;
       // part group indices are global to this round
-      call_after_round(call, rv.data());
+      call_after_round(call, rv);
     }
   }
   t_retry = ms_since(tr);

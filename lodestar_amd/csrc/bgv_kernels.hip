@@ -24,6 +24,7 @@
 #define BGV_KERNEL_SIDE 1
 #include "bls_hash.h"
 #include "bls_pairing.h"
+#include "bls_team.h"
 
 // Waves per SIMD the verify kernels are register-budgeted for (1: up to 512 VGPRs).
 #ifndef BGV_WPE
@@ -174,11 +175,61 @@ __global__ void BGV_KATTR k_reduce(const bgv_dgroup* __restrict__ groups, const 
   if (j == 0) fg[blockIdx.x] = mf;
 }
 
-// Group closing: final exponentiation of the group product, verdict = (result == 1).
+// Group closing, team-parallel (bls_team.h): a team of 16 lanes per group, lane c < 12
+// owning one Fp coefficient of the running value; operands exchanged through LDS.
+__constant__ fp2_t kTeamFrob1[6] = BGV_FROB1;
+__constant__ fp_t kTeamFrob2[6] = BGV_FROB2;
+
+struct tm_dev_ops {
+  fp_t* A;  // this team's 12 + 12 LDS slots
+  fp_t* B;
+  int c;   // lane within the team, 0..15
+  int cc;  // component computed by this lane (lanes 12..15 duplicate 8..11)
+  __device__ fp_t mul(const fp_t& x, const fp_t& y) {
+    if (c < BGV_TEAM_COMPS) {
+      A[c] = x;
+      B[c] = y;
+    }
+    __syncthreads();
+    const fp_t r = tm_mul_lane(cc, A, B);
+    __syncthreads();
+    return r;
+  }
+  __device__ fp_t sqr(const fp_t& x) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t r = tm_mul_lane(cc, A, A);
+    __syncthreads();
+    return r;
+  }
+  __device__ fp_t conj(const fp_t& x) { return fp_select(((cc >> 1) & 1) != 0, x, fp_neg(x)); }
+  __device__ fp_t frob(const fp_t& x) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t x0 = A[cc & ~1], x1 = A[cc | 1];
+    __syncthreads();
+    return tm_frob_lane(cc, x0, x1, kTeamFrob1[tm_tower_pos(cc)]);
+  }
+  __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(cc)]); }
+  __device__ bool is_fp6(const fp_t& x) {
+    const bool bad = c < BGV_TEAM_COMPS && ((cc >> 1) & 1) && !fp_is_zero(x);
+    const uint64_t m = __ballot(bad);
+    return ((m >> (threadIdx.x & ~(BGV_TEAM - 1))) & 0xffffu) == 0;
+  }
+};
+
+#define BGV_FINAL_TEAMS (64 / BGV_TEAM)
 __global__ void BGV_KATTR k_final(uint32_t ngroups, const fp12_t* __restrict__ fg, int32_t* __restrict__ verdict) {
-  const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= ngroups) return;
-  verdict[gi] = fp12_is_one(final_exp(fg[gi])) ? 1 : 0;
+  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
+  const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
+  // teams past the end duplicate the last group so every lane reaches every barrier
+  const uint32_t g = gi < ngroups ? gi : ngroups - 1;
+  const fp_t x = reinterpret_cast<const fp_t*>(fg + g)[tm_fp_index(cc)];
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  const bool one = tm_final_exp_is_one(o, x);
+  if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
 __global__ void k_aggregate_cached(const uint32_t* __restrict__ idx, uint32_t n, const g1_aff* __restrict__ cache,
@@ -317,7 +368,8 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
   hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.fg);
   BGV_MARK(5);
   BGV_MARK(6);
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.fg, b.verdict);
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.ngroups, b.fg,
+                     b.verdict);
   BGV_MARK(7);
   return hipGetLastError();
 }

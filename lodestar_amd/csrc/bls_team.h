@@ -1,0 +1,196 @@
+// Team-parallel Fp12 arithmetic for the group closing (final exponentiation).
+//
+// The per-set kernels keep one signature set per lane: thousands of independent
+// chains fill the chip.  A group closing is different: one final exponentiation
+// per device group, a few thousand groups per launch, each a serial chain of
+// ~340 Fp12 squarings/products.  Run one lane per group and the closing is
+// latency-bound (one wave per SIMD, a third of the SIMDs busy).  Here a TEAM of
+// 16 lanes owns one Fp12 value: lane c < 12 holds one Fp coefficient in the
+// w-basis,
+//
+//     f = sum_{k<6} f_k w^k,  w^6 = xi = 1 + u,  f_k = re + im u,  c = 2k + (re ? 0 : 1)
+//
+// (tower position of w^k: k even -> c0.c[k/2], k odd -> c1.c[k/2]), and a product
+// is computed coefficient-parallel: lane (k, e) accumulates the 12 double-width
+// Fp products that make up its coefficient (negations folded into operands as
+// 2p - x, so every term is positive) and does ONE Montgomery reduction.  Operands
+// are exchanged through LDS.  Per lane that is 12 x 196 + 196 u32 MACs against
+// 54 full Fp products (~21k MACs) for the one-lane tower product.
+//
+// Final exponentiation without an inversion.  f^((p^12-1)/r) == 1 iff
+// f^((p^2+1) h) lies in Fp6 (the kernel of x -> x^(p^6-1)), h = (p^4-p^2+1)/r.
+// Modulo Fp6*, conj(a) = a^(p^6) = N(a)/a is an inverse of a for EVERY a, and the
+// Frobenius maps are automorphisms, so the x-chain of the hard part
+// (bls_pairing.h final_exp) runs unchanged on representatives with generic
+// squarings, starting from t = frob2(f) * f; the verdict is "odd w-coefficients of
+// the result are zero".  The easy part's Fp12 inversion disappears.
+#pragma once
+#include "bls_pairing.h"
+
+#define BGV_TEAM 16
+#define BGV_TEAM_COMPS 12
+
+// fp_t index inside fp12_t of w-basis component c
+BGV_HD int tm_fp_index(int c) {
+  const int k = c >> 1, e = c & 1;
+  return 2 * ((k & 1) * 3 + (k >> 1)) + e;
+}
+
+// a + b with carries normalized and no reduction (a, b < 2p -> < 4p < 2^392)
+BGV_HD fp_t fp_add_norm(const fp_t& a, const fp_t& b) {
+  fp_t r;
+  uint32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    const uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & LMASK;
+    c = s >> LBITS;
+  }
+  return r;
+}
+
+// t += x * y over 2 NL columns.  With limbs < 2^28 each column takes < 2^56 per
+// term and 14 terms per product: 12 products stay below 2^63.4.
+BGV_HD void wide_mac(uint64_t* t, const fp_t& x, const fp_t& y) {
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    BGV_UNROLL for (int j = 0; j < NL; ++j) t[i + j] += (uint64_t)x.v[i] * y.v[j];
+  }
+}
+
+// Montgomery reduction of a double-width column sum T < 96 p^2 -> T / 2^392 mod p,
+// result < 1.07 p (weakly reduced).  Same rows as fp_sqr_l's reduction.
+BGV_HD fp_t wide_redc(uint64_t* t) {
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    const uint32_t m = ((uint32_t)t[i] * BGV_N0) & LMASK;
+    BGV_UNROLL for (int j = 0; j < NL; ++j) t[i + j] += (uint64_t)m * P_[j];
+    t[i + 1] += t[i] >> LBITS;
+  }
+  fp_t r;
+  BGV_UNROLL for (int j = 0; j < NL - 1; ++j) {
+    r.v[j] = (uint32_t)t[NL + j] & LMASK;
+    t[NL + j + 1] += t[NL + j] >> LBITS;
+  }
+  r.v[NL - 1] = (uint32_t)t[2 * NL - 1];
+  return r;
+}
+
+// Coefficient c = 2k + e of a * b (A, B: the 12 w-basis components of each factor).
+//   c_k = sum_{i+j=k} a_i b_j + xi sum_{i+j=k+6} a_i b_j,  xi (y0 + y1 u) = (y0 - y1) + (y0 + y1) u
+// re(a_i b_j) = x0 y0 + (-x1) y1        im(a_i b_j) = x0 y1 + x1 y0
+// re(xi a_i b_j) = x0 (y0 - y1) + (-x1)(y0 + y1)    im(xi a_i b_j) = x0 (y0 + y1) + x1 (y0 - y1)
+BGV_HD fp_t tm_mul_lane(int c, const fp_t* A, const fp_t* B) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int q = 0; q < 2 * NL; ++q) t[q] = 0;
+  BGV_NO_UNROLL for (int i = 0; i < 6; ++i) {
+    const bool wrap = i > k;
+    const int j = wrap ? k + 6 - i : k - i;
+    const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+    const fp_t y0 = B[2 * j], y1 = B[2 * j + 1];
+    const fp_t d = fp_sub_nr(y0, y1);    // y0 - y1 + 2p in (0, 4p)
+    const fp_t s = fp_add_norm(y0, y1);  // < 4p
+    const fp_t x1n = fp_sub_nr(fp_zero(), x1);  // 2p - x1 in (0, 2p]
+    const fp_t X2 = fp_select(e != 0, x1n, x1);
+    const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+    const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+    wide_mac(t, x0, Y1);
+    wide_mac(t, X2, Y2);
+  }
+  return wide_redc(t);
+}
+
+// Frobenius (p-power) on the component pair (x0, x1) = f_k:
+// frob(f)_k = conj(f_k) * g_k, g = BGV_FROB1 indexed by tower position.
+BGV_HD fp_t tm_frob_lane(int c, const fp_t& x0, const fp_t& x1, const fp2_t& g) {
+  const int e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int q = 0; q < 2 * NL; ++q) t[q] = 0;
+  // (x0 - x1 u)(g0 + g1 u) = (x0 g0 + x1 g1) + (x0 g1 - x1 g0) u
+  wide_mac(t, x0, fp_select(e != 0, g.c0, g.c1));
+  wide_mac(t, fp_select(e != 0, x1, fp_sub_nr(fp_zero(), x1)), fp_select(e != 0, g.c1, g.c0));
+  return wide_redc(t);
+}
+
+BGV_HD int tm_tower_pos(int c) {
+  const int k = c >> 1;
+  return (k & 1) * 3 + (k >> 1);
+}
+
+// The hard-part x-chain on representatives modulo Fp6* (see the header).  O supplies
+// mul, sqr, conj, frob, frob2, is_fp6 on its element type E.
+template <class O, class E>
+BGV_HD E tm_pow_x(O& o, const E& a) {
+  const uint64_t X = BGV_X_ABS;
+  E r = a;
+  BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {
+    r = o.sqr(r);
+    if ((X >> i) & 1) r = o.mul(r, a);
+  }
+  return o.conj(r);  // x < 0
+}
+
+template <class O, class E>
+BGV_HD bool tm_final_exp_is_one(O& o, const E& f) {
+  const E t = o.mul(o.frob2(f), f);               // f^(p^2 + 1)
+  E a = o.mul(tm_pow_x(o, t), o.conj(t));         // t^(x-1)
+  a = o.mul(tm_pow_x(o, a), o.conj(a));           // t^((x-1)^2)
+  a = o.mul(tm_pow_x(o, a), o.frob(a));           // ^(x+p)
+  E b = tm_pow_x(o, tm_pow_x(o, a));              // a^(x^2)
+  b = o.mul(o.mul(b, o.frob2(a)), o.conj(a));     // a^(x^2 + p^2 - 1)
+  const E t3 = o.mul(o.sqr(t), t);                // t^3
+  return o.is_fp6(o.mul(b, t3));
+}
+
+// Host emulation of a team (tests): all 12 components in one value, every op
+// runs the lane functions above for each lane.
+struct tm_emu_t {
+  fp_t c[BGV_TEAM_COMPS];
+};
+
+struct tm_emu_ops {
+  BGV_HD tm_emu_t mul(const tm_emu_t& a, const tm_emu_t& b) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_mul_lane(c, a.c, b.c);
+    return r;
+  }
+  BGV_HD tm_emu_t sqr(const tm_emu_t& a) { return mul(a, a); }
+  BGV_HD tm_emu_t conj(const tm_emu_t& a) {
+    tm_emu_t r = a;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      if ((c >> 1) & 1) r.c[c] = fp_neg(a.c[c]);
+    return r;
+  }
+  BGV_HD tm_emu_t frob(const tm_emu_t& a) {
+    const fp2_t g[6] = BGV_FROB1;
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      r.c[c] = tm_frob_lane(c, a.c[c & ~1], a.c[c | 1], g[tm_tower_pos(c)]);
+    return r;
+  }
+  BGV_HD tm_emu_t frob2(const tm_emu_t& a) {
+    const fp_t g[6] = BGV_FROB2;
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = fp_mul(a.c[c], g[tm_tower_pos(c)]);
+    return r;
+  }
+  BGV_HD bool is_fp6(const tm_emu_t& a) {
+    bool z = true;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      if ((c >> 1) & 1) z = z && fp_is_zero(a.c[c]);
+    return z;
+  }
+};
+
+BGV_HD tm_emu_t tm_emu_from_fp12(const fp12_t& f) {
+  const fp_t* v = reinterpret_cast<const fp_t*>(&f);
+  tm_emu_t r;
+  for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = v[tm_fp_index(c)];
+  return r;
+}
+
+BGV_HD fp12_t tm_emu_to_fp12(const tm_emu_t& a) {
+  fp12_t f;
+  fp_t* v = reinterpret_cast<fp_t*>(&f);
+  for (int c = 0; c < BGV_TEAM_COMPS; ++c) v[tm_fp_index(c)] = a.c[c];
+  return f;
+}

@@ -8,6 +8,7 @@
 
 #include "../../lodestar_amd/csrc/bls_hash.h"
 #include "../../lodestar_amd/csrc/bls_pairing.h"
+#include "../../lodestar_amd/csrc/bls_team.h"
 
 static fp_t in_fp(const uint8_t* be) { return fp_to_mont(fp_from_be48(be)); }
 static void out_fp(uint8_t* be, const fp_t& a) { fp_to_be48(be, fp_from_mont(a)); }
@@ -180,6 +181,28 @@ void hs_miller_loop2(uint8_t* out, const uint8_t* p1, const uint8_t* q1, const u
                      int two) {
   out_fp12(out, miller_loop2(in_g1(p1), in_g2(q1), in_g1(p2), in_g2(q2), two != 0));
 }
+// team-parallel closing arithmetic (bls_team.h), emulated lane by lane
+void hs_team_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul(tm_emu_from_fp12(in_fp12(a)), tm_emu_from_fp12(in_fp12(b)))));
+}
+void hs_team_frob(uint8_t* r, const uint8_t* a) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.frob(tm_emu_from_fp12(in_fp12(a)))));
+}
+void hs_team_conj(uint8_t* r, const uint8_t* a) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.conj(tm_emu_from_fp12(in_fp12(a)))));
+}
+void hs_team_frob2(uint8_t* r, const uint8_t* a) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.frob2(tm_emu_from_fp12(in_fp12(a)))));
+}
+int hs_team_final_is_one(const uint8_t* f) {
+  tm_emu_ops o;
+  return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
+}
+int hs_final_is_one(const uint8_t* f) { return fp12_is_one(final_exp(in_fp12(f))); }
 // per-set path of k_prep's pk task + k_miller for one single set: r pk, r (-G1) via the
 // shared-inversion affine conversion, then the 2-pair loop and the final exponentiation
 int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* sig_aff, uint64_t r) {

@@ -1,0 +1,120 @@
+"""BASELINE.json configurations at full size on the GPU, checked through
+properties that do not need the oracle at that size: every verdict is known by
+construction (device-signed with interop keys, then corrupted in known places),
+aggregate signatures are signatures by the summed secret key, and the pubkey
+aggregates are pinned against the oracle on a few committees.
+
+  config 1  128 single sets, one job, per-job mode (BlsSingleThreadVerifier)
+  config 2  1024 aggregate sets x 128 distinct pubkeys (contiguous committees), 8 x 128-set jobs
+  config 4  8192 batchable one-set jobs, 1 % corrupted (random.Random(0x8192).sample), and one call
+  config 5  one rank's shard of the epoch sweep: a 1,048,576-key device cache, 131,072 single sets
+"""
+import hashlib
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def interop_sk_int(i):
+    """state-transition/src/util/interop.ts:19-22"""
+    return int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R
+
+
+def sk_bytes(k):
+    return k.to_bytes(32, "big")
+
+
+@pytest.fixture(scope="module")
+def big():
+    """Context with 1,048,576 interop validators in the device cache."""
+    from lodestar_amd import native
+    c = native.Context()
+    n = 1 << 20
+    sks = [interop_sk_int(i) for i in range(n)]
+    for lo in range(0, n, 1 << 17):
+        c.keygen(b"".join(sk_bytes(k) for k in sks[lo:lo + (1 << 17)]), cache_first=lo, want_pubkeys=False)
+    assert c.pubkeys_count() == n
+    yield c, sks
+    c.close()
+
+
+def test_config1_single_thread_job(big):
+    from lodestar_amd import native
+    c, sks = big
+    idx = list(range(1000, 1128))
+    msgs = [hashlib.sha256(b"config1-%d" % i).digest() for i in idx]
+    sigs = c.sign(b"".join(sk_bytes(sks[i]) for i in idx), b"".join(msgs))
+    sets = [native.SetSpec(msgs[j], sigs[96 * j:96 * j + 96], pk_indices=[i]) for j, i in enumerate(idx)]
+    assert c.verify_jobs([(sets, False)], native.MODE_PER_JOB) == [1]
+    sets[77] = native.SetSpec(msgs[76], sets[77].sig, pk_indices=[idx[77]])
+    assert c.verify_jobs([(sets, False)], native.MODE_PER_JOB) == [0]
+
+
+def test_config2_aggregates(big):
+    """1024 committees of 128 contiguous validators; committee c signs root_c with
+    sum(sk) mod r.  Jobs of 128 sets (multithread/index.ts:155-166)."""
+    from lodestar_amd import native
+    from oracle import bls12381 as o  # pins two pubkey aggregates
+    c, sks = big
+    ncomm, size = 1024, 128
+    roots = [hashlib.sha256(b"lodestar-bench" + c_.to_bytes(4, "little")).digest() for c_ in range(ncomm)]
+    agg_sk = [sum(sks[size * q:size * q + size]) % R for q in range(ncomm)]
+    sigs = c.sign(b"".join(sk_bytes(k) for k in agg_sk), b"".join(roots))
+    for q in (0, 777):
+        members = list(range(size * q, size * q + size))
+        assert c.aggregate_pubkeys(members) == o.g1_serialize(o.sk_to_pk(agg_sk[q]))
+    sets = [native.SetSpec(roots[q], sigs[96 * q:96 * q + 96], pk_indices=list(range(size * q, size * q + size)))
+            for q in range(ncomm)]
+    jobs = [(sets[j:j + 128], True) for j in range(0, ncomm, 128)]
+    assert c.verify_jobs(jobs, native.MODE_WORKER) == [1] * 8
+    # a committee missing one member -> its job false; the other 7 true (retry isolates it)
+    q = 300
+    sets[q] = native.SetSpec(roots[q], sets[q].sig, pk_indices=list(range(size * q, size * q + size - 1)))
+    jobs = [(sets[j:j + 128], True) for j in range(0, ncomm, 128)]
+    assert c.verify_jobs(jobs, native.MODE_WORKER) == [1, 1, 0, 1, 1, 1, 1, 1]
+
+
+def _gossip(c, sks, n, base, seed):
+    from lodestar_amd import native
+    key_of = [(base + i * 7919) % len(sks) for i in range(n)]
+    msgs = [hashlib.sha256(b"lodestar-bench" + i.to_bytes(4, "little")).digest() for i in range(n)]
+    sigs = c.sign(b"".join(sk_bytes(sks[k]) for k in key_of), b"".join(msgs))
+    sigs = [sigs[96 * i:96 * i + 96] for i in range(n)]
+    expect = [1] * n
+    bad = random.Random(seed).sample(range(n), int(round(n * 0.01)))
+    for j, i in enumerate(bad):
+        if j % 3 == 0:
+            msgs[i] = hashlib.sha256(b"wrong" + msgs[i]).digest()
+            expect[i] = 0
+        elif j % 3 == 1:
+            key_of[i] = (key_of[i] + 1) % len(sks)
+            expect[i] = 0
+        else:
+            sigs[i] = bytes([sigs[i][0] & 0x7F]) + sigs[i][1:]
+            expect[i] = -1
+    sets = [native.SetSpec(msgs[i], sigs[i], pk_indices=[key_of[i]]) for i in range(n)]
+    return sets, expect
+
+
+def test_config4_gossip_8192(big):
+    from lodestar_amd import native
+    c, sks = big
+    sets, expect = _gossip(c, sks, 8192, 0, 0x8192)
+    st = native.BgvStats()
+    assert c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER, st) == expect
+    assert st.batch_retries > 0
+    # mode (ii): one call holding all 8192 sets -> rejects with the first error code
+    assert c.verify_jobs([(sets, True)], native.MODE_WORKER) == [-1]
+
+
+def test_config5_shard_of_epoch_sweep(big):
+    """Rank 0's 131,072 of 1,048,576 sets over the full 2^20-key cache (indices spread
+    over all of it), 1 % corrupted; verdicts by construction."""
+    from lodestar_amd import native
+    c, sks = big
+    sets, expect = _gossip(c, sks, 1 << 17, 12345, 0x5)
+    assert c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER) == expect

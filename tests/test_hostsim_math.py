@@ -280,3 +280,43 @@ def test_verify_one_two_pair(L):
     assert L.hs_verify_one(hs.g1_b(pk), hs.g2_b(h), hs.g2_b(sig), r) == 1
     other = o.sign(o.interop_secret_key(6), msg)
     assert L.hs_verify_one(hs.g1_b(pk), hs.g2_b(h), hs.g2_b(other), r) == 0
+
+
+def rf12():
+    return hs.fp12_b_tower([rfp() for _ in range(12)])
+
+
+def test_team_fp12_ops(L):
+    """Coefficient-parallel Fp12 product / Frobenius maps (bls_team.h) against the
+    tower formulas, including operands with limbs at the 2p bound."""
+    two_p_minus_1 = hs.fp12_b_tower([P - 1] * 12)
+    for a, b in [(rf12(), rf12()) for _ in range(6)] + [(two_p_minus_1, two_p_minus_1)]:
+        want, got = hs.buf(576), hs.buf(576)
+        L.hs_fp12_mul(want, a, b)
+        L.hs_team_mul(got, a, b)
+        assert got.raw == want.raw
+        for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
+            tf(got, a)
+            ref(want, a)
+            assert got.raw == want.raw
+        L.hs_team_conj(got, a)
+        assert hs.b_fp12_tower(got.raw) == hs.b_fp12_tower(a)[:6] + [(-x) % P for x in hs.b_fp12_tower(a)[6:]]
+
+
+def test_team_final_exp_check(L):
+    """The inversion-free quotient check agrees with final_exp(f) == 1: random f
+    (not 1) and f = e(P, Q) e(-P, Q) Miller values (1), and a perturbed product."""
+    for _ in range(2):
+        f = rf12()
+        assert L.hs_final_is_one(f) == 0
+        assert L.hs_team_final_is_one(f) == 0
+    p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    q = g2_rand_in_group()
+    m = hs.buf(576)
+    L.hs_miller_loop2(m, hs.g1_b(p), hs.g2_b(q), hs.g1_b(o.g1_neg(p)), hs.g2_b(q), 1)
+    assert L.hs_final_is_one(m.raw) == 1
+    assert L.hs_team_final_is_one(m.raw) == 1
+    q2 = g2_rand_in_group()
+    L.hs_miller_loop2(m, hs.g1_b(p), hs.g2_b(q), hs.g1_b(o.g1_neg(p)), hs.g2_b(q2), 1)
+    assert L.hs_final_is_one(m.raw) == 0
+    assert L.hs_team_final_is_one(m.raw) == 0
