@@ -215,10 +215,15 @@ def main():
         groups = statistics.mean(s.device_groups for s in stats)
         pipeline_macs = (sum(per_set.values()) * slots + per_group * groups) * MACS_PER_FP_MUL * args.steps * world
         pipeline_frac = pipeline_macs / elapsed / (PEAK_MAC_PER_S * world)
-        traffic = None
+        # HBM bytes per launch of the dominant kernel from the committed PMC passes
+        # (profiles/traffic.json, per slot) scaled to this run's slots per launch
+        traffic = hbm_gbs = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
-            traffic = json.load(open(tf)).get(dom)
+            per_slot = json.load(open(tf)).get(dom, {}).get("bytes_per_slot")
+            if per_slot:
+                traffic = per_slot * slots_per_launch
+                hbm_gbs = traffic / (avg[dom] * 1e-3) / 1e9
         line = {
             "metric": "verified signature sets/sec (node) at 8192-set batches",
             "value": total_sets / elapsed,
@@ -248,6 +253,8 @@ def main():
                          "unit": "TMAC/s (u32 mad)", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
                          "work_per_set": "%d Fp-mul-eq x %d MAC" % (per_set[dom], MACS_PER_FP_MUL),
                          "sets_per_launch": slots_per_launch, "ms_per_launch": avg[dom],
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "hbm_GBps": hbm_gbs, "hbm_frac_of_8TBps": hbm_gbs / 8000 if hbm_gbs else None,
                          "pipeline_frac": pipeline_frac},
             "setup_s": setup_s,
         }

@@ -123,6 +123,19 @@ BGV_HD fp_t fp_add_nr(const fp_t& a, const fp_t& b) {
   return r;
 }
 
+// a + b with the carries propagated and no reduction: normalized limbs (< 2^28),
+// value < A + B.  For Karatsuba operand sums that only ever feed a product.
+BGV_HD fp_t fp_add_norm(const fp_t& a, const fp_t& b) {
+  fp_t r;
+  uint32_t c = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    const uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & LMASK;
+    c = s >> LBITS;
+  }
+  return r;
+}
+
 BGV_HD fp_t fp_add(const fp_t& a, const fp_t& b) {
   fp_t r;
   uint32_t c = 0;
@@ -181,9 +194,11 @@ BGV_HD fp_t fp_neg(const fp_t& a) {
   return fp_select(nz == 0, r, a);
 }
 
-// Montgomery product, row-wise over 28-bit limbs (R = 2^392).  Each of the 14
-// u64 accumulators receives at most 2 products per row (< 2^58 + 2^56) over
-// 14 rows plus carries: < 2^63, so no carry ever leaves an accumulator early.
+// Montgomery product, row-wise over 28-bit limbs (R = 2^392).  Operand limbs may
+// be < 2^29 (an unreduced fp_add_nr): each of the 14 u64 accumulators receives at
+// most 2 products per row (< 2^58 + 2^56) over <= 14 rows plus carries, < 2^62.2,
+// so no carry ever leaves an accumulator early.  Operand VALUES may be up to 16p
+// each: the result is < 256 p^2 / R + p < 1.1 p, weakly reduced.
 // The out-of-line products take their limbs as 28 / 14 scalar arguments: the
 // AMDGPU calling convention passes those in VGPRs v0..v27, whereas a second
 // struct argument would travel through scratch memory on every call.
@@ -394,16 +409,24 @@ BGV_HD fp2_t fp2_dbl(const fp2_t& a) { return fp2_t{fp_dbl(a.c0), fp_dbl(a.c1)};
 BGV_HD fp2_t fp2_neg(const fp2_t& a) { return fp2_t{fp_neg(a.c0), fp_neg(a.c1)}; }
 BGV_HD fp2_t fp2_conj(const fp2_t& a) { return fp2_t{a.c0, fp_neg(a.c1)}; }
 
+// Operand components: normalized limbs, values < 8p (fp6/fp12 Karatsuba sums made
+// with fp2_add_norm); the operand sums below are then < 16p with limbs < 2^29,
+// within fp_mul_l's bounds.  The result is weakly reduced.
 BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   fp_t t0 = fp_mul(a.c0, b.c0);
   fp_t t1 = fp_mul(a.c1, b.c1);
-  fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  fp_t t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));
   return fp2_t{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
+// a weakly reduced (< 2p): (a0 + a1)(a0 - a1 + 2p) and (2 a0) a1, no reduced adds.
 BGV_HD fp2_t fp2_sqr(const fp2_t& a) {
-  fp_t t = fp_mul(a.c0, a.c1);
-  return fp2_t{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+  return fp2_t{fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_nr(a.c0, a.c1)), fp_mul(fp_add_nr(a.c0, a.c0), a.c1)};
+}
+
+// Karatsuba operand sum: normalized, unreduced (< 4p for reduced inputs)
+BGV_HD fp2_t fp2_add_norm(const fp2_t& a, const fp2_t& b) {
+  return fp2_t{fp_add_norm(a.c0, b.c0), fp_add_norm(a.c1, b.c1)};
 }
 
 BGV_HD fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { return fp2_t{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
@@ -470,13 +493,17 @@ BGV_HD fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) {
 BGV_HD fp6_t fp6_neg(const fp6_t& a) { return fp6_t{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 BGV_HD fp6_t fp6_mul_v(const fp6_t& a) { return fp6_t{fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
+// Operand coefficients: normalized, values < 4p (an fp6_add_norm of reduced values
+// at most); the result is weakly reduced.
 BGV_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
   fp2_t t0 = fp2_mul(a.c0, b.c0);
   fp2_t t1 = fp2_mul(a.c1, b.c1);
   fp2_t t2 = fp2_mul(a.c2, b.c2);
-  fp2_t c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
-  fp2_t c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
-  fp2_t c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  fp2_t c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a.c1, a.c2), fp2_add_norm(b.c1, b.c2)), t1), t2)),
+                     t0);
+  fp2_t c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a.c0, a.c1), fp2_add_norm(b.c0, b.c1)), t0), t1),
+                     fp2_mul_xi(t2));
+  fp2_t c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a.c0, a.c2), fp2_add_norm(b.c0, b.c2)), t0), t2), t1);
   return fp6_t{c0, c1, c2};
 }
 
@@ -500,7 +527,7 @@ BGV_NOINLINE fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) 
   fp2_t t0 = fp2_mul(a.c0, b0);
   fp2_t t1 = fp2_mul(a.c1, b1);
   fp2_t c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), t0);
-  fp2_t c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  fp2_t c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a.c0, a.c1), fp2_add_norm(b0, b1)), t0), t1);
   fp2_t c2 = fp2_add(fp2_mul(a.c2, b0), t1);
   return fp6_t{c0, c1, c2};
 }
@@ -535,17 +562,21 @@ BGV_HD bool fp12_is_one(const fp12_t& a) {
 
 BGV_HD fp12_t fp12_conj(const fp12_t& a) { return fp12_t{a.c0, fp6_neg(a.c1)}; }
 
+BGV_HD fp6_t fp6_add_norm(const fp6_t& a, const fp6_t& b) {
+  return fp6_t{fp2_add_norm(a.c0, b.c0), fp2_add_norm(a.c1, b.c1), fp2_add_norm(a.c2, b.c2)};
+}
+
 BGV_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
   fp6_t t0 = fp6_mul(a.c0, b.c0);
   fp6_t t1 = fp6_mul(a.c1, b.c1);
-  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_norm(a.c0, a.c1), fp6_add_norm(b.c0, b.c1)), t0), t1);
   fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
   return fp12_t{c0, c1};
 }
 
 BGV_NOINLINE fp12_t fp12_sqr(const fp12_t& a) {
   fp6_t t = fp6_mul(a.c0, a.c1);
-  fp6_t s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6_t s = fp6_mul(fp6_add_norm(a.c0, a.c1), fp6_add_norm(a.c0, fp6_mul_v(a.c1)));
   fp6_t c0 = fp6_sub(fp6_sub(s, t), fp6_mul_v(t));
   return fp12_t{c0, fp6_add(t, t)};
 }
@@ -555,7 +586,7 @@ BGV_NOINLINE fp12_t fp12_sqr(const fp12_t& a) {
 BGV_NOINLINE fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
   fp6_t t0 = fp6_mul_01(f.c0, l0, l1);
   fp6_t t1 = fp6_mul_1(f.c1, l3);
-  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), l0, fp2_add(l1, l3)), t0), t1);
+  fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add_norm(f.c0, f.c1), l0, fp2_add_norm(l1, l3)), t0), t1);
   fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
   return fp12_t{c0, c1};
 }

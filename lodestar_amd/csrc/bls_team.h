@@ -36,18 +36,6 @@ BGV_HD int tm_fp_index(int c) {
   return 2 * ((k & 1) * 3 + (k >> 1)) + e;
 }
 
-// a + b with carries normalized and no reduction (a, b < 2p -> < 4p < 2^392)
-BGV_HD fp_t fp_add_norm(const fp_t& a, const fp_t& b) {
-  fp_t r;
-  uint32_t c = 0;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    const uint32_t s = a.v[i] + b.v[i] + c;
-    r.v[i] = s & LMASK;
-    c = s >> LBITS;
-  }
-  return r;
-}
-
 // t += x * y over 2 NL columns.  With limbs < 2^28 each column takes < 2^56 per
 // term and 14 terms per product: 12 products stay below 2^63.4.
 BGV_HD void wide_mac(uint64_t* t, const fp_t& x, const fp_t& y) {
