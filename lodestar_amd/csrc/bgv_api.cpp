@@ -120,7 +120,7 @@ struct Pinned {
 struct Exec {
   hipStream_t main = nullptr;   // per-set kernels (compute-bound)
   hipStream_t close = nullptr;  // group closing + retry rounds (latency-bound): high priority
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_sets = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_prep = nullptr, ev_sets = nullptr;
   hipEvent_t kev[2 * BGV_NKERNELS] = {};
   void* slot_mem = nullptr;
   uint32_t slot_cap = 0;
@@ -360,6 +360,7 @@ static int exec_create(Exec* x) {
   HIPCHK(hipEventCreate(&x->ev0));
   HIPCHK(hipEventCreate(&x->ev1));
   HIPCHK(hipEventCreateWithFlags(&x->ev_sets, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&x->ev_prep, hipEventDisableTiming));
   for (auto& e : x->kev) HIPCHK(hipEventCreate(&e));
   return BGV_OK;
 }
@@ -379,6 +380,7 @@ static void exec_destroy(Exec* x) {
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
   if (x->ev_sets) (void)hipEventDestroy(x->ev_sets);
+  if (x->ev_prep) (void)hipEventDestroy(x->ev_prep);
   for (auto& e : x->kev)
     if (e) (void)hipEventDestroy(e);
   if (x->close) (void)hipStreamSynchronize(x->close);
@@ -697,19 +699,24 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   bgv_streams SC{x.close, prof ? x.kev : nullptr};
   int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;
   {
-    // One super-batch at a time runs the compute-bound per-set kernels; the
-    // latency-bound group closing of one batch then overlaps the next batch's
-    // per-set kernels (dispatchers stagger instead of running in lockstep).
+    // One super-batch at a time runs k_prep (the token); the token passes on as
+    // soon as k_prep is done, so the next batch's k_prep waves queue behind this
+    // batch's k_miller and take each SIMD as a Miller wave retires (no drain
+    // bubble between batches).  The latency-bound group closing runs on the
+    // high-priority stream and overlaps both.
     const auto tt = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> tok(*d.compute_mu);
     t_tok = ms_since(tt);
     HIPCHK(hipEventRecord(x.ev0, x.main));
-    HIPCHK(bgv_launch_sets(b, S));
+    HIPCHK(bgv_launch_prep(b, S));
+    HIPCHK(hipEventRecord(x.ev_prep, x.main));
+    HIPCHK(bgv_launch_miller(b, S));
     HIPCHK(hipEventRecord(x.ev_sets, x.main));
-    HIPCHK(hipEventSynchronize(x.ev_sets));
+    HIPCHK(hipEventSynchronize(x.ev_prep));
     t_sets = ms_since(tt) - t_tok;
   }
   const auto tg = std::chrono::steady_clock::now();
+  HIPCHK(hipStreamWaitEvent(x.close, x.ev_sets, 0));
   HIPCHK(bgv_launch_groups(b, SC));
   HIPCHK(hipEventRecord(x.ev1, x.close));
   HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));

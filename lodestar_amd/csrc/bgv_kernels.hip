@@ -344,7 +344,7 @@ static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 // then k_miller.  Kernel k is bracketed by events kev[2k], kev[2k+1] when profiling.
 #define BGV_MARK(i) \
   if (s.kev) (void)hipEventRecord(s.kev[i], s.main)
-hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
+hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
   BGV_MARK(0);
@@ -352,11 +352,22 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
                      b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.rg,
                      b.pk_status);
   BGV_MARK(1);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
+  const uint32_t n = b.nslots;
+  if (n == 0) return hipSuccess;
   BGV_MARK(2);
   hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.rg, b.sig,
                      b.sig_status, b.pk_status, b.f);
   BGV_MARK(3);
   return hipGetLastError();
+}
+
+hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
+  hipError_t e = bgv_launch_prep(b, s);
+  return e != hipSuccess ? e : bgv_launch_miller(b, s);
 }
 
 // Per-group kernels over b.groups (contiguous slot ranges of <= 64 slots): used for

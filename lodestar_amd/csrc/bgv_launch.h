@@ -48,7 +48,9 @@ struct bgv_streams {
   hipStream_t main;
   hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr
 };
-hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);
+hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // prep + miller
+hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
+hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s);
 size_t bgv_slot_bytes();
 size_t bgv_group_bytes();
