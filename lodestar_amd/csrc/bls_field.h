@@ -294,12 +294,39 @@ BGV_HD fp_t fp_from_mont(const fp_t& a) {
   return fp_canon(fp_mul(a, one));
 }
 
-// a^e for a fixed (lane-uniform) exponent given as 32-bit little-endian words.
-BGV_HD fp_t fp_pow_words(const fp_t& a, const uint32_t* e, int nbits) {
-  fp_t r = a;  // the top bit of every exponent used here is 1
-  BGV_NO_UNROLL for (int i = nbits - 2; i >= 0; --i) {
-    r = fp_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+// a^e for a fixed (lane-uniform) exponent given as 32-bit little-endian words:
+// left-to-right sliding window of width 5 over a table of the 16 odd powers
+// a, a^3, ..., a^31.  The exponents used here have ~229 one bits in 381: the
+// window cuts the products from ~229 to ~84 (16 of them for the table).  All
+// control flow follows the exponent, so a wave never diverges.
+BGV_HD uint32_t exp_bit(const uint32_t* e, int i) { return (e[i >> 5] >> (i & 31)) & 1u; }
+
+BGV_NOINLINE fp_t fp_pow_words(const fp_t& a, const uint32_t* e, int nbits) {
+  fp_t tab[16];
+  tab[0] = a;
+  const fp_t a2 = fp_sqr(a);
+  BGV_NO_UNROLL for (int k = 1; k < 16; ++k) tab[k] = fp_mul(tab[k - 1], a2);
+  fp_t r = a;
+  bool started = false;
+  int i = nbits - 1;
+  BGV_NO_UNROLL while (i >= 0) {
+    if (!exp_bit(e, i)) {
+      r = fp_sqr(r);  // only reached once started: the top bit is 1
+      --i;
+      continue;
+    }
+    int j = i - 4 > 0 ? i - 4 : 0;
+    while (!exp_bit(e, j)) ++j;
+    uint32_t w = 0;
+    for (int q = i; q >= j; --q) w = (w << 1) | exp_bit(e, q);
+    if (started) {
+      BGV_NO_UNROLL for (int q = i; q >= j; --q) r = fp_sqr(r);
+      r = fp_mul(r, tab[w >> 1]);
+    } else {
+      r = tab[w >> 1];
+      started = true;
+    }
+    i = j - 1;
   }
   return r;
 }
