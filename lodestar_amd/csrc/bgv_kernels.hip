@@ -66,14 +66,12 @@ __device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ 
   sig_status[s] = st;
 }
 
-__device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* __restrict__ h) {
+__device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
   const bgv_dslot& d = slots[s];
   if (d.flags & BGV_SLOT_PAD) return;
   uint8_t msg[32];
   for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
-  g2_aff a;
-  jac_to_aff(&a, hash_to_g2(msg, 32));
-  h[s] = a;
+  h[s] = hash_to_g2(msg, 32);  // stays Jacobian: k_miller adds it with miller_add_jq
 }
 
 __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
@@ -124,7 +122,7 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_aff* __restrict__ sig,
-                                 int32_t* __restrict__ sig_status, g2_aff* __restrict__ h,
+                                 int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
                                  const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                  const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
                                  g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status) {
@@ -143,7 +141,7 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
 // take part (padding, failed decode/aggregation).  An infinity signature keeps
 // its pubkey pair and drops the signature pair, as blst's accumulator does.
 __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                   const g1_aff* __restrict__ rpk, const g2_aff* __restrict__ h,
+                                   const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
                                    const g1_aff* __restrict__ rg, const g2_aff* __restrict__ sig,
                                    const int32_t* __restrict__ sig_status, const int32_t* __restrict__ pk_status,
                                    fp12_t* __restrict__ f) {
@@ -387,7 +385,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
 #undef BGV_MARK
 
 size_t bgv_slot_bytes() {
-  return 2 * sizeof(g2_aff) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
+  return sizeof(g2_aff) + sizeof(g2_jac) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
 }
 size_t bgv_group_bytes() { return sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
@@ -396,8 +394,8 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   uint8_t* p = static_cast<uint8_t*>(slot_mem);
   b->sig = reinterpret_cast<g2_aff*>(p);
   p += sizeof(g2_aff) * (size_t)cap_slots;
-  b->h = reinterpret_cast<g2_aff*>(p);
-  p += sizeof(g2_aff) * (size_t)cap_slots;
+  b->h = reinterpret_cast<g2_jac*>(p);
+  p += sizeof(g2_jac) * (size_t)cap_slots;
   b->rpk = reinterpret_cast<g1_aff*>(p);
   p += sizeof(g1_aff) * (size_t)cap_slots;
   b->rg = reinterpret_cast<g1_aff*>(p);

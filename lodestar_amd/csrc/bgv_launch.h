@@ -27,7 +27,7 @@ struct bgv_dev_batch {
   const uint8_t* pk_bytes;
   // carved per-slot / per-group scratch
   aff_t<fp2_t>* sig;  // decompressed signatures
-  aff_t<fp2_t>* h;    // H(m_i)
+  jac_t<fp2_t>* h;    // H(m_i), Jacobian
   aff_t<fp_t>* rpk;   // r_i * aggregated pubkey
   aff_t<fp_t>* rg;    // r_i * (-G1)
   fp12_t* f;          // per-slot 2-pair Miller loop value

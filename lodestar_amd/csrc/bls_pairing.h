@@ -76,11 +76,56 @@ BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
   return fp12_conj(f);
 }
 
+// Addition step with a Jacobian Q = (X2 : Y2 : Z2) (no affine conversion of Q):
+// T <- T + Q, and the chord line at P scaled by Z2^3 (an Fp2 factor, killed by the
+// final exponentiation):  l0 = r X2 Z2 - Y2 Z3,  l1 = -r Z2^3 xP,  l3 = Z3 Z2^3 yP.
+// q.zz = Z2^2, q.zzz_xn = -Z2^3 xP, q.zzz_yp = Z2^3 yP, q.xz = X2 Z2 are per-pair constants.
+struct miller_jq {
+  g2_jac q;
+  fp2_t zz, xz, zzz_xn, zzz_yp;
+};
+
+BGV_HD miller_jq miller_jq_make(const g2_jac& q, const fp_t& xp_neg, const fp_t& yp) {
+  miller_jq r;
+  r.q = q;
+  r.zz = fp2_sqr(q.z);
+  const fp2_t zzz = fp2_mul(r.zz, q.z);
+  r.xz = fp2_mul(q.x, q.z);
+  r.zzz_xn = fp2_mul_fp(zzz, xp_neg);
+  r.zzz_yp = fp2_mul_fp(zzz, yp);
+  return r;
+}
+
+BGV_NOINLINE void miller_add_jq(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const miller_jq& c) {
+  fp2_t ZZ = fp2_sqr(t.z);
+  fp2_t U1 = fp2_mul(t.x, c.zz);
+  fp2_t U2 = fp2_mul(c.q.x, ZZ);
+  fp2_t S1 = fp2_mul(t.y, fp2_mul(c.zz, c.q.z));
+  fp2_t S2 = fp2_mul(c.q.y, fp2_mul(t.z, ZZ));
+  fp2_t H = fp2_sub(U2, U1);
+  fp2_t HH = fp2_sqr(H);
+  fp2_t I = fp2_dbl(fp2_dbl(HH));
+  fp2_t J = fp2_mul(H, I);
+  fp2_t r = fp2_dbl(fp2_sub(S2, S1));
+  fp2_t V = fp2_mul(U1, I);
+  fp2_t X3 = fp2_sub(fp2_sub(fp2_sqr(r), J), fp2_dbl(V));
+  fp2_t Y3 = fp2_sub(fp2_mul(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul(S1, J)));
+  fp2_t Z3 = fp2_mul(fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.z, c.q.z)), ZZ), c.zz), H);
+  *l0 = fp2_sub(fp2_mul(r, c.xz), fp2_mul(c.q.y, Z3));
+  *l1 = fp2_mul(r, c.zzz_xn);
+  *l3 = fp2_mul(Z3, c.zzz_yp);
+  t.x = X3;
+  t.y = Y3;
+  t.z = Z3;
+}
+
 // f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) (conjugated) with one shared accumulator: the
 // squarings of f are paid once for both pairs.  two == false drops the second pair.
-BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_aff& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
+// Q1 (= H(m)) is Jacobian: its additions use miller_add_jq, saving the inversion.
+BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
   const fp_t xn1 = fp_neg(p1.x), xn2 = fp_neg(p2.x);
-  g2_jac t1 = jac_from_aff(q1), t2 = jac_from_aff(q2);
+  const miller_jq c1 = miller_jq_make(q1, xn1, p1.y);
+  g2_jac t1 = q1, t2 = jac_from_aff(q2);
   fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
   miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
@@ -91,7 +136,7 @@ BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_aff& q1, const g1_af
   }
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
-      miller_add(t1, &l0, &l1, &l3, q1, xn1, p1.y);
+      miller_add_jq(t1, &l0, &l1, &l3, c1);
       f = fp12_mul_line(f, l0, l1, l3);
       if (two) {
         miller_add(t2, &l0, &l1, &l3, q2, xn2, p2.y);

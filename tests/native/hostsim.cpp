@@ -52,10 +52,7 @@ int hs_k_sig_body(const uint8_t* sig96) {
   if (g2_decompress(&a, &inf, sig96) || inf) return 0;
   return g2_in_subgroup(jac_from_aff(a));
 }
-int hs_k_hash_body(const uint8_t* msg32) {
-  g2_aff a;
-  return jac_to_aff(&a, hash_to_g2(msg32, 32));
-}
+int hs_k_hash_body(const uint8_t* msg32) { return !jac_is_inf(hash_to_g2(msg32, 32)); }
 int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_aff p = in_g1(pk_aff_tl);
   g1_jac acc = jac_infinity<fp_t>();
@@ -67,7 +64,7 @@ int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   return 1;
 }
 void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
-  (void)miller_loop2(in_g1(p), in_g2(q), g1_neg_generator(), in_g2(q), true);
+  (void)miller_loop2(in_g1(p), jac_from_aff(in_g2(q)), g1_neg_generator(), in_g2(q), true);
 }
 void hs_k_final_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
 void hs_k_reduce_step(const uint8_t* f) { (void)fp12_mul(in_fp12(f), in_fp12(f)); }
@@ -179,7 +176,12 @@ void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12
 void hs_final_exp(uint8_t* out, const uint8_t* f) { out_fp12(out, final_exp(in_fp12(f))); }
 void hs_miller_loop2(uint8_t* out, const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2,
                      int two) {
-  out_fp12(out, miller_loop2(in_g1(p1), in_g2(q1), in_g1(p2), in_g2(q2), two != 0));
+  // Q1 handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
+  const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};
+  const g2_aff a = in_g2(q1);
+  const fp2_t l2 = fp2_sqr(l);
+  const g2_jac q1j = {fp2_mul(a.x, l2), fp2_mul(a.y, fp2_mul(l2, l)), l};
+  out_fp12(out, miller_loop2(in_g1(p1), q1j, in_g1(p2), in_g2(q2), two != 0));
 }
 // team-parallel closing arithmetic (bls_team.h), emulated lane by lane
 void hs_team_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {
@@ -210,7 +212,7 @@ int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* si
   const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), r);
   g1_aff pa, ga;
   jac2_to_aff(&pa, &ga, a, g);
-  return fp12_is_one(final_exp(miller_loop2(pa, in_g2(h_aff), ga, in_g2(sig_aff), true)));
+  return fp12_is_one(final_exp(miller_loop2(pa, jac_from_aff(in_g2(h_aff)), ga, in_g2(sig_aff), true)));
 }
 
 int hs_g1_decompress(uint8_t* out, const uint8_t* in48) {
