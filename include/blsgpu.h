@@ -143,6 +143,31 @@ int bgv_aggregate_pubkeys(bgv_ctx* ctx, const uint32_t* indices, size_t n, uint8
  * (x.c1 | x.c0 | y.c1 | y.c0). */
 int bgv_hash_to_g2(bgv_ctx* ctx, const uint8_t* msgs, const uint32_t* lens, size_t n, uint8_t* out192);
 
+/* SURVEY 8(f) rows beside the verify path -------------------------------- */
+
+/* Deposit-time pubkey validation: bls.PublicKey.fromBytes(pubkey, CoordType.affine,
+ * validate=true) (state-transition/src/block/processDeposit.ts:64) for n 48-byte
+ * compressed keys.  out_status[i] = 0 or -BLST code (BAD_ENCODING, POINT_NOT_ON_CURVE,
+ * PK_IS_INFINITY, POINT_NOT_IN_GROUP).  out96 (may be NULL) receives the 96-byte
+ * uncompressed record of every valid key (bgv_pubkeys_put / bgv_set.pk_bytes format). */
+int bgv_pubkeys_validate(bgv_ctx* ctx, const uint8_t* keys48, size_t n, int32_t* out_status, uint8_t* out96);
+
+/* Op-pool signature aggregation: bls.Signature.aggregate(sigs.map(s =>
+ * Signature.fromBytes(s, undefined, true))) (chain/opPools/attestationPool.ts:184-187,
+ * aggregatedAttestationPool.ts:319-321, syncCommitteeMessagePool.ts:126-129,
+ * syncContributionAndProofPool.ts:181-185).  naggs aggregates over consecutive runs of
+ * counts[a] signatures (96-byte records, lens[i] = the received length).  out96[a] is the
+ * compressed aggregate, out_status[a] 0, -BLST code of the first signature that fails,
+ * or -BGV_E_EMPTY_AGGREGATE for an empty run. */
+int bgv_aggregate_signatures(bgv_ctx* ctx, const uint8_t* sigs96, const uint32_t* lens, const uint32_t* counts,
+                             size_t naggs, uint8_t* out96, int32_t* out_status);
+
+/* Deposit signature check (processDeposit.ts:62-70): key validated as above, then
+ * Signature.fromBytes(sig, affine, true).verify(pk, signingRoot); any BLS error counts
+ * as invalid.  out_valid[i] = 1 or 0. */
+int bgv_deposits_verify(bgv_ctx* ctx, const uint8_t* keys48, const uint8_t* msgs32, const uint8_t* sigs96, size_t n,
+                        int32_t* out_valid);
+
 /* Bench/test utilities (not part of IBlsVerifier): derive public keys and sign on
  * the device.  sks are n x 32-byte big-endian secret keys (SecretKey.fromBytes).
  * bgv_keygen writes n x 48-byte compressed pubkeys to out48 (may be NULL) and, when

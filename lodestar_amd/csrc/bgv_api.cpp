@@ -1051,6 +1051,115 @@ int bgv_hash_to_g2(bgv_ctx* c, const uint8_t* msgs, const uint32_t* lens, size_t
   return BGV_OK;
 }
 
+int bgv_pubkeys_validate(bgv_ctx* c, const uint8_t* keys48, size_t n, int32_t* out_status, uint8_t* out96) {
+  if (!c || (n && (!keys48 || !out_status))) return -BGV_E_ARG;
+  if (c->closed) return -BGV_E_CLOSED;
+  if (n == 0) return BGV_OK;
+  std::lock_guard<std::mutex> lk(c->util_mu);
+  Device& d = c->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  uint8_t *dk = nullptr, *dout = nullptr;
+  int32_t* dst = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dk), 48 * n));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dout), 96 * n));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dst), 4 * n));
+  HIPCHK(hipMemcpyAsync(dk, keys48, 48 * n, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(bgv_launch_pk_validate(dk, (uint32_t)n, dst, dout, d.stream));
+  HIPCHK(hipMemcpyAsync(out_status, dst, 4 * n, hipMemcpyDeviceToHost, d.stream));
+  if (out96) HIPCHK(hipMemcpyAsync(out96, dout, 96 * n, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  (void)hipFree(dk);
+  (void)hipFree(dout);
+  (void)hipFree(dst);
+  for (size_t i = 0; i < n; ++i) out_status[i] = -out_status[i];
+  return BGV_OK;
+}
+
+int bgv_aggregate_signatures(bgv_ctx* c, const uint8_t* sigs96, const uint32_t* lens, const uint32_t* counts,
+                             size_t naggs, uint8_t* out96, int32_t* out_status) {
+  if (!c || (naggs && (!counts || !out96 || !out_status))) return -BGV_E_ARG;
+  if (c->closed) return -BGV_E_CLOSED;
+  if (naggs == 0) return BGV_OK;
+  std::vector<uint32_t> first(naggs);
+  size_t n = 0;
+  for (size_t a = 0; a < naggs; ++a) {
+    first[a] = (uint32_t)n;
+    n += counts[a];
+  }
+  if (n && (!sigs96 || !lens)) return -BGV_E_ARG;
+  std::vector<int32_t> st(n);
+  std::lock_guard<std::mutex> lk(c->util_mu);
+  Device& d = c->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  uint8_t *ds = nullptr, *dout = nullptr;
+  uint32_t *dl = nullptr, *df = nullptr, *dc = nullptr;
+  int32_t* dst = nullptr;
+  void* pts = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&ds), 96 * n + 1));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dl), 4 * n + 4));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dst), 4 * n + 4));
+  HIPCHK(hipMalloc(&pts, bgv_g2_point_bytes() * n + 1));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&df), 4 * naggs));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dc), 4 * naggs));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dout), 96 * naggs));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(ds, sigs96, 96 * n, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(dl, lens, 4 * n, hipMemcpyHostToDevice, d.stream));
+  }
+  HIPCHK(hipMemcpyAsync(df, first.data(), 4 * naggs, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(hipMemcpyAsync(dc, counts, 4 * naggs, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(bgv_launch_sig_aggregate(ds, dl, (uint32_t)n, df, dc, (uint32_t)naggs, pts, dst, dout, d.stream));
+  if (n) HIPCHK(hipMemcpyAsync(st.data(), dst, 4 * n, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(out96, dout, 96 * naggs, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  void* bufs[] = {ds, dl, dst, pts, df, dc, dout};
+  for (void* b : bufs) (void)hipFree(b);
+  // verdict per aggregate: the first signature (in order) that fails to decode or
+  // validate, as Signature.fromBytes throws on it; [] -> EMPTY_AGGREGATE_ARRAY
+  for (size_t a = 0; a < naggs; ++a) {
+    int32_t code = counts[a] ? BGV_OK : -BGV_E_EMPTY_AGGREGATE;
+    for (uint32_t k = 0; k < counts[a] && code == BGV_OK; ++k)
+      if (st[first[a] + k] != BGV_OK) code = -st[first[a] + k];
+    out_status[a] = code;
+    if (code != BGV_OK) memset(out96 + 96 * a, 0, 96);
+  }
+  return BGV_OK;
+}
+
+int bgv_deposits_verify(bgv_ctx* c, const uint8_t* keys48, const uint8_t* msgs32, const uint8_t* sigs96, size_t n,
+                        int32_t* out_valid) {
+  if (!c || (n && (!keys48 || !msgs32 || !sigs96 || !out_valid))) return -BGV_E_ARG;
+  if (n == 0) return BGV_OK;
+  std::vector<int32_t> ks(n);
+  std::vector<uint8_t> pk96(96 * n);
+  int rc = bgv_pubkeys_validate(c, keys48, n, ks.data(), pk96.data());
+  if (rc) return rc;
+  // every deposit with a valid key is its own job (Signature.verify per deposit)
+  std::vector<bgv_set> sets;
+  std::vector<bgv_job> jobs;
+  std::vector<size_t> which;
+  for (size_t i = 0; i < n; ++i) {
+    out_valid[i] = 0;
+    if (ks[i] != BGV_OK) continue;
+    bgv_set st{};
+    st.n_pk = 1;
+    st.sig_len = 96;
+    st.pk_bytes = pk96.data() + 96 * i;
+    st.msg = msgs32 + 32 * i;
+    st.sig = sigs96 + 96 * i;
+    jobs.push_back(bgv_job{(uint32_t)sets.size(), 1, 0});
+    sets.push_back(st);
+    which.push_back(i);
+  }
+  if (jobs.empty()) return BGV_OK;
+  std::vector<int32_t> codes(jobs.size());
+  rc = bgv_verify(c, jobs.data(), jobs.size(), sets.data(), sets.size(), BGV_MODE_PER_JOB, codes.data(), nullptr);
+  if (rc) return rc;
+  // processDeposit.ts:62-70 catches every BLS error: anything but "valid" is invalid
+  for (size_t k = 0; k < which.size(); ++k) out_valid[which[k]] = codes[k] == 1 ? 1 : 0;
+  return BGV_OK;
+}
+
 int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48) {
   if (!c || (n && !sks)) return -BGV_E_ARG;
   if (c->closed) return -BGV_E_CLOSED;

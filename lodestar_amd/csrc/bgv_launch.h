@@ -64,3 +64,9 @@ hipError_t bgv_launch_hash(const uint8_t* msgs, const uint32_t* offs, const uint
                            uint8_t* out192, hipStream_t st);
 hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st);
 hipError_t bgv_launch_sign(const uint8_t* sks, const uint8_t* msgs, uint32_t n, uint8_t* out96, hipStream_t st);
+hipError_t bgv_launch_pk_validate(const uint8_t* keys48, uint32_t n, int32_t* status, uint8_t* out96,
+                                  hipStream_t st);
+hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens, uint32_t n, const uint32_t* first,
+                                    const uint32_t* count, uint32_t naggs, void* pts, int32_t* status,
+                                    uint8_t* out96, hipStream_t st);
+size_t bgv_g2_point_bytes();

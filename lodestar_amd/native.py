@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = [
     "bgv_init", "bgv_close", "bgv_destroy", "bgv_pubkeys_put", "bgv_pubkeys_count", "bgv_verify",
     "bgv_verify_async", "bgv_aggregate_pubkeys", "bgv_hash_to_g2", "bgv_keygen", "bgv_sign",
     "bgv_set_rng_seed", "bgv_strerror", "bgv_device_count", "bgv_profile",
+    "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify",
 ]
 
 
@@ -101,6 +102,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_strerror": ([ctypes.c_int], ctypes.c_char_p),
             "bgv_device_count": ([], ctypes.c_int),
             "bgv_profile": ([P, ctypes.c_int, P, P, ctypes.c_int, P], ctypes.c_int),
+            "bgv_pubkeys_validate": ([P, P, SZ, P, P], ctypes.c_int),
+            "bgv_aggregate_signatures": ([P, P, P, P, SZ, P, P], ctypes.c_int),
+            "bgv_deposits_verify": ([P, P, P, P, SZ, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -214,6 +218,34 @@ class Context:
         out = ctypes.create_string_buffer(192 * len(msgs))
         _check(self.lib.bgv_hash_to_g2(self._h, _buf(b"".join(msgs)), lens, len(msgs), out))
         return [out.raw[192 * i:192 * i + 192] for i in range(len(msgs))]
+
+    # --- deposit keys, op-pool aggregation, deposit signatures ----
+    def pubkeys_validate(self, keys48: Sequence[bytes]):
+        """PublicKey.fromBytes(pk, affine, validate=true) per key -> (codes, uncompressed)."""
+        n = len(keys48)
+        st = (ctypes.c_int32 * max(1, n))()
+        out = ctypes.create_string_buffer(96 * max(1, n))
+        _check(self.lib.bgv_pubkeys_validate(self._h, _buf(b"".join(keys48)), n, st, out))
+        return list(st[:n]), [out.raw[96 * i:96 * i + 96] for i in range(n)]
+
+    def aggregate_signatures(self, aggregates: Sequence[Sequence[bytes]]):
+        """Signature.aggregate over each list of signatures -> [(code, compressed96)]."""
+        sigs = [s for agg in aggregates for s in agg]
+        counts = (ctypes.c_uint32 * max(1, len(aggregates)))(*[len(a) for a in aggregates])
+        lens = (ctypes.c_uint32 * max(1, len(sigs)))(*[len(x) for x in sigs])
+        raw = b"".join(bytes(x[:96]).ljust(96, b"\0") for x in sigs)
+        out = ctypes.create_string_buffer(96 * max(1, len(aggregates)))
+        st = (ctypes.c_int32 * max(1, len(aggregates)))()
+        _check(self.lib.bgv_aggregate_signatures(self._h, _buf(raw), lens, counts, len(aggregates), out, st))
+        return [(st[a], out.raw[96 * a:96 * a + 96]) for a in range(len(aggregates))]
+
+    def deposits_verify(self, keys48: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> List[int]:
+        n = len(keys48)
+        assert len(msgs) == n and len(sigs) == n and all(len(x) == 96 for x in sigs)
+        out = (ctypes.c_int32 * max(1, n))()
+        _check(self.lib.bgv_deposits_verify(self._h, _buf(b"".join(keys48)), _buf(b"".join(msgs)),
+                                            _buf(b"".join(sigs)), n, out))
+        return list(out[:n])
 
     # --- verification -------------------------------------------------------
     def verify_jobs(self, jobs, mode: int = MODE_WORKER, stats: Optional[BgvStats] = None) -> List[int]:

@@ -860,3 +860,54 @@ def chunkify_maximize_chunk_size(arr, min_per_chunk: int):
         return [list(arr)]
     per_chunk = -(-len(arr) // chunk_count)
     return [list(arr[i:i + per_chunk]) for i in range(0, len(arr), per_chunk)]
+
+
+# ----------------------------------------------------------------------------
+# deposit-time key validation, op-pool signature aggregation
+# ----------------------------------------------------------------------------
+def pubkey_validate(b: bytes) -> int:
+    """bls.PublicKey.fromBytes(pubkey, CoordType.affine, validate=true)
+    (state-transition/src/block/processDeposit.ts:64): ZCash decode, then blst's
+    key validation — infinity -> BLST_PK_IS_INFINITY, outside G1 ->
+    BLST_POINT_NOT_IN_GROUP.  Returns 0 or the BLST code."""
+    try:
+        pt = g1_decompress(b)
+    except BlstError as e:
+        return e.code
+    if pt is None:
+        return BLST_PK_IS_INFINITY
+    if not g1_in_group(pt):
+        return BLST_POINT_NOT_IN_GROUP
+    return 0
+
+
+def signatures_aggregate(sigs):
+    """bls.Signature.aggregate(sigs.map(s => Signature.fromBytes(s, undefined, true)))
+    (chain/opPools/attestationPool.ts:184-187, aggregatedAttestationPool.ts:319-321,
+    syncCommitteeMessagePool.ts:126-129, syncContributionAndProofPool.ts:181-185).
+    Returns (0, compressed 96 B) or (code, None): the first failing signature's
+    BLST code, 20 (EMPTY_AGGREGATE_ARRAY) for [].  An infinity signature decodes
+    and adds nothing (dependency-defined; unpinned here)."""
+    if len(sigs) == 0:
+        return 20, None
+    acc = None
+    for s in sigs:
+        try:
+            acc = g2_add(acc, signature_from_bytes(s, True))
+        except BlstError as e:
+            return e.code, None
+    return 0, g2_compress(acc)
+
+
+def deposit_valid(pk48: bytes, msg32: bytes, sig96: bytes) -> bool:
+    """processDeposit.ts:62-70: key validated, signature validated and verified;
+    any BLS error counts as invalid (the catch-all returns)."""
+    if pubkey_validate(pk48) != 0:
+        return False
+    try:
+        sig = signature_from_bytes(sig96, True)
+    except BlstError:
+        return False
+    if sig is None:
+        return False
+    return core_verify(g1_decompress(pk48), msg32, sig)

@@ -211,3 +211,30 @@ def test_blsgpuverifier_e2e():
         c.close()
 
     asyncio.run(run())
+
+
+def test_pubkeys_validate_golden(ctx):
+    """Deposit-time key validation (processDeposit.ts:64) against tests/golden/next.json."""
+    cases = load("next.json")["pubkeys"]
+    codes, recs = ctx.pubkeys_validate([bytes.fromhex(c["pk"]) for c in cases])
+    assert codes == [-c["expect"] for c in cases]
+    keys = load("keys.json")
+    for i in range(8):  # valid keys come back as the uncompressed cache record
+        assert recs[i].hex() == keys["pk_uncompressed"][i]
+
+
+def test_aggregate_signatures_golden(ctx):
+    """Op-pool Signature.aggregate over validated signatures, golden aggregates."""
+    cases = load("next.json")["aggregates"]
+    got = ctx.aggregate_signatures([[bytes.fromhex(s) for s in c["sigs"]] for c in cases])
+    for c, (code, agg) in zip(cases, got):
+        assert code == -c["expect"], c
+        if c["expect"] == 0:
+            assert agg.hex() == c["aggregate"]
+
+
+def test_deposits_verify_golden(ctx):
+    cases = load("next.json")["deposits"]
+    got = ctx.deposits_verify([bytes.fromhex(c["pk"]) for c in cases], [bytes.fromhex(c["msg"]) for c in cases],
+                              [bytes.fromhex(c["sig"]) for c in cases])
+    assert got == [c["expect"] for c in cases]

@@ -92,3 +92,20 @@ def test_batch_semantics():
         assert False
     except o.BlstError as e:
         assert "BLST_INVALID_SIZE" in str(e)
+
+
+def test_next_rows_oracle(golden_dir):
+    """Oracle restatements for SURVEY 8(f): every reference interop pubkey
+    (state-transition/test-cache/interop-pubkeys.json) passes deposit validation;
+    the committed next.json fixtures agree with the oracle."""
+    import json
+    import os
+    ref = json.load(open(os.path.join(golden_dir, "interop-pubkeys.json")))
+    for h in ref[:16]:
+        assert o.pubkey_validate(bytes.fromhex(h[2:])) == 0
+    nxt = json.load(open(os.path.join(golden_dir, "next.json")))
+    for c in nxt["pubkeys"]:
+        assert o.pubkey_validate(bytes.fromhex(c["pk"])) == c["expect"]
+    for c in nxt["aggregates"][:5]:
+        code, agg = o.signatures_aggregate([bytes.fromhex(s) for s in c["sigs"]])
+        assert code == c["expect"] and (agg.hex() if agg else None) == c["aggregate"]
