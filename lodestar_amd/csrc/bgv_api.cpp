@@ -144,6 +144,7 @@ struct Device {
   int id = 0;
   hipStream_t stream = nullptr;      // utility work (cache upload, hooks, keygen)
   bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
+  void* gtab = nullptr;               // fixed-base multiples of -G1 (built at init)
   size_t cache_cap = 0;
   std::vector<Exec*> execs;
   // held while one super-batch runs its per-set kernels (pointer: Device stays movable)
@@ -410,6 +411,7 @@ static bgv_dev_batch make_batch(Device& d, Exec& x, uint32_t nslots, uint32_t ng
   b.groups = x.d_groups;
   b.pk_idx = x.d_idx;
   b.cache_opaque = d.cache;
+  b.gtab = d.gtab;
   b.pk_bytes = x.d_pkb;
   bgv_carve(&b, x.slot_mem, x.slot_cap, x.group_mem, x.group_cap);
   return b;
@@ -841,6 +843,8 @@ static void ctx_free_devices(bgv_ctx* c) {
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
+    if (d.gtab) (void)hipFree(d.gtab);
+    d.gtab = nullptr;
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.stream = nullptr;
   }
@@ -858,7 +862,9 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     Device& d = c->devs[i];
     d.id = (devices && ndev > 0) ? devices[i] : 0;
     bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
-              hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
+              hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&d.gtab, bgv_gtab_bytes()) == hipSuccess && bgv_launch_gtab(d.gtab, d.stream) == hipSuccess &&
+              hipStreamSynchronize(d.stream) == hipSuccess;
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
       Exec* x = new Exec();
       d.execs.push_back(x);

@@ -77,7 +77,8 @@ __device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__
 __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                     g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status) {
+                                     g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
+                                     const g1_aff* __restrict__ gtab) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
   if (d.flags & BGV_SLOT_PAD) {
@@ -108,8 +109,9 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
     if (jac_is_inf(a)) {
       st = BGV_ST_INFINITY;
     } else {
-      // r_i * (-G1) for the signature's pair; never infinity (0 < r_i < group order)
-      const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), d.scalar);
+      // r_i * (-G1) for the signature's pair from the fixed-base table; never infinity
+      // (0 < r_i < group order)
+      const g1_jac g = g1_neg_gen_mul(gtab, d.scalar);
       g1_aff pa, ga;
       jac2_to_aff(&pa, &ga, a, g);
       rpk[s] = pa;
@@ -125,7 +127,8 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
                                  int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
                                  const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                  const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                 g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status) {
+                                 g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
+                                 const g1_aff* __restrict__ gtab) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   // hash first: the longest task starts earliest
@@ -134,7 +137,7 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
   else if (blockIdx.y == 1)
     task_sig(s, slots, sig, sig_status);
   else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status);
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status, gtab);
 }
 
 // f_i = MillerLoop(r pk, H(m)) * MillerLoop(-r G1, sig); 1 for slots that do not
@@ -326,6 +329,11 @@ __global__ void BGV_KATTR k_sig_sum(const uint32_t* __restrict__ first, const ui
   }
 }
 
+__global__ void k_gtab_build(g1_aff* __restrict__ tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < BGV_GTAB_ENTRIES) tab[i] = g1_gtab_entry(i);
+}
+
 __global__ void k_hash_msgs(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ offs,
                             const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ out192) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -432,7 +440,7 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   BGV_MARK(0);
   hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.sig, b.sig_status, b.h,
                      b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.rg,
-                     b.pk_status);
+                     b.pk_status, reinterpret_cast<const g1_aff*>(b.gtab));
   BGV_MARK(1);
   return hipGetLastError();
 }
@@ -541,6 +549,11 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
   return hipGetLastError();
 }
 size_t bgv_g2_point_bytes() { return sizeof(g2_jac); }
+size_t bgv_gtab_bytes() { return sizeof(g1_aff) * BGV_GTAB_ENTRIES; }
+hipError_t bgv_launch_gtab(void* tab, hipStream_t st) {
+  hipLaunchKernelGGL(k_gtab_build, dim3(BGV_GTAB_ENTRIES / 64), dim3(64), 0, st, reinterpret_cast<g1_aff*>(tab));
+  return hipGetLastError();
+}
 
 hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st) {
   if (n == 0) return hipSuccess;

@@ -25,6 +25,7 @@ struct bgv_dev_batch {
   const uint32_t* pk_idx;
   const bgv_cache_entry* cache_opaque;
   const uint8_t* pk_bytes;
+  const void* gtab;  // fixed-base table of multiples of -G1 (bgv_launch_gtab)
   // carved per-slot / per-group scratch
   aff_t<fp2_t>* sig;  // decompressed signatures
   jac_t<fp2_t>* h;    // H(m_i), Jacobian
@@ -70,3 +71,5 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
                                     const uint32_t* count, uint32_t naggs, void* pts, int32_t* status,
                                     uint8_t* out96, hipStream_t st);
 size_t bgv_g2_point_bytes();
+size_t bgv_gtab_bytes();
+hipError_t bgv_launch_gtab(void* tab, hipStream_t st);

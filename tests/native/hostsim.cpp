@@ -39,6 +39,23 @@ static void out_g1(uint8_t* be, const g1_aff& a) {
   out_fp(be + 48, a.y);
 }
 
+// host copy of the device's fixed-base table (k_gtab_build), built on first use
+static const g1_aff* host_gtab() {
+  static g1_aff* tab = nullptr;
+  if (!tab) {
+#ifdef BGV_COUNT_OPS
+    const unsigned long long m = bgv_count_mul, q = bgv_count_sqr;
+#endif
+    tab = new g1_aff[BGV_GTAB_ENTRIES];
+    for (int i = 0; i < BGV_GTAB_ENTRIES; ++i) tab[i] = g1_gtab_entry(i);
+#ifdef BGV_COUNT_OPS
+    bgv_count_mul = m;  // one-time table build is not per-set work
+    bgv_count_sqr = q;
+#endif
+  }
+  return tab;
+}
+
 extern "C" {
 #ifdef BGV_COUNT_OPS
 unsigned long long bgv_count_mul = 0, bgv_count_sqr = 0;
@@ -58,7 +75,7 @@ int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
   const g1_jac a = jac_mul_u64(acc, r);
-  const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), r);
+  const g1_jac g = g1_neg_gen_mul(host_gtab(), r);
   g1_aff pa, ga;
   jac2_to_aff(&pa, &ga, a, g);
   return 1;
@@ -140,6 +157,8 @@ int hs_g2_psi(uint8_t* out, const uint8_t* a) { return g2_out(out, g2_psi(jac_fr
 int hs_g2_clear_cofactor(uint8_t* out, const uint8_t* a) {
   return g2_out(out, g2_clear_cofactor(jac_from_aff(in_g2(a))));
 }
+// r * (-G1) via the fixed-base table (task_pk)
+int hs_g1_neg_gen_mul(uint8_t* out, uint64_t r) { return g1_out(out, g1_neg_gen_mul(host_gtab(), r)); }
 int hs_g1_mul_u64(uint8_t* out, const uint8_t* aff, uint64_t k) {
   return g1_out(out, jac_mul_u64(jac_from_aff(in_g1(aff)), k));
 }

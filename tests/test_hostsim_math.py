@@ -323,3 +323,12 @@ def test_team_final_exp_check(L):
     L.hs_miller_loop2(m, hs.g1_b(p), hs.g2_b(q), hs.g1_b(o.g1_neg(p)), hs.g2_b(q2), 1)
     assert L.hs_final_is_one(m.raw) == 0
     assert L.hs_team_final_is_one(m.raw) == 0
+
+
+def test_fixed_base_neg_g1(L):
+    """task_pk's table-driven r * (-G1) equals the oracle's scalar multiple."""
+    neg = o.g1_neg(o.G1)
+    for r in [1, 2, 255, 256, 0xFFFFFFFFFFFFFFFF, 0x8000000000000000] + [rnd.getrandbits(64) | 1 for _ in range(6)]:
+        out = hs.buf(96)
+        assert L.hs_g1_neg_gen_mul(out, hs.ctypes.c_uint64(r)) == 1
+        assert hs.b_g1(out.raw) == o.g1_mul(neg, r)
