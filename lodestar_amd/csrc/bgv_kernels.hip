@@ -10,8 +10,8 @@
 //                   r_i * (-G1), both made affine with one shared inversion
 //   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)) * MillerLoop(-r_i G1, sig_i), one
 //              shared Fp12 accumulator (2-pair loop)
-//   k_reduce   per device group (one wavefront): prod f_i via an LDS tree
-//   k_final    per group: final exponentiation -> == 1
+//   k_final    per device group (a team of 16 lanes): prod f_i over the group's
+//              slots, then the final-exponentiation check -> == 1
 //
 // This is the randomized batch equation of blst's verifyMultipleAggregateSignatures
 // (called from packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25):
@@ -158,24 +158,6 @@ __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t
   f[s] = r;
 }
 
-// One wavefront per device group: LDS tree of Fp12 products.
-__global__ void BGV_KATTR k_reduce(const bgv_dgroup* __restrict__ groups, const fp12_t* __restrict__ f,
-                                   fp12_t* __restrict__ fg) {
-  extern __shared__ uint32_t lds[];
-  fp12_t* lf = reinterpret_cast<fp12_t*>(lds);
-  const bgv_dgroup g = groups[blockIdx.x];
-  const uint32_t j = threadIdx.x;
-  fp12_t mf = fp12_one();
-  if (j < g.n_slots) mf = f[g.first_slot + j];
-  for (uint32_t d = 1; d < BGV_WAVE; d <<= 1) {
-    lf[j] = mf;
-    __syncthreads();
-    if ((j & (2 * d - 1)) == 0 && j + d < g.n_slots) mf = fp12_mul(mf, lf[j + d]);
-    __syncthreads();
-  }
-  if (j == 0) fg[blockIdx.x] = mf;
-}
-
 // Group closing, team-parallel (bls_team.h): a team of 16 lanes per group, lane c < 12
 // owning one Fp coefficient of the running value; operands exchanged through LDS.
 __constant__ fp2_t kTeamFrob1[6] = BGV_FROB1;
@@ -220,15 +202,35 @@ struct tm_dev_ops {
 };
 
 #define BGV_FINAL_TEAMS (64 / BGV_TEAM)
-__global__ void BGV_KATTR k_final(uint32_t ngroups, const fp12_t* __restrict__ fg, int32_t* __restrict__ verdict) {
+// One team per device group: the product of the group's per-slot f_i (coefficient-
+// parallel team products, operands straight from the per-slot array), then the
+// final-exponentiation check.  The teams of a wave loop to the wave's longest group,
+// the shorter ones multiplying by 1, so every lane reaches every barrier.
+__global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                  const fp12_t* __restrict__ f, int32_t* __restrict__ verdict) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  __shared__ uint32_t lens[BGV_FINAL_TEAMS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
-  // teams past the end duplicate the last group so every lane reaches every barrier
-  const uint32_t g = gi < ngroups ? gi : ngroups - 1;
-  const fp_t x = reinterpret_cast<const fp_t*>(fg + g)[tm_fp_index(cc)];
+  // teams past the end duplicate the last group
+  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  if (c == 0) lens[team] = g.n_slots;
+  __syncthreads();
+  uint32_t nmax = 0;
+  BGV_UNROLL for (int t = 0; t < BGV_FINAL_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
+  const int fi = tm_fp_index(cc);
+  const fp_t one_c = cc == 0 ? fp_one() : fp_zero();  // component cc of 1
+  const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
+  constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
   tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  fp_t x = g.n_slots ? fs[fi] : one_c;
+  fp_t y = 1 < g.n_slots ? fs[kFp12 + fi] : one_c;
+  BGV_NO_UNROLL for (uint32_t k = 1; k < nmax; ++k) {
+    const fp_t yn = k + 1 < g.n_slots ? fs[kFp12 * (k + 1) + fi] : one_c;  // next operand in flight
+    x = o.mul(x, y);
+    y = yn;
+  }
   const bool one = tm_final_exp_is_one(o, x);
   if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
 }
@@ -464,14 +466,10 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
 // the first pass and, over the same per-slot results, for the per-job retry pass.
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
   if (b.ngroups == 0) return hipSuccess;
-  const size_t lds = BGV_WAVE * sizeof(fp12_t);
   BGV_MARK(4);
-  hipLaunchKernelGGL(k_reduce, dim3(b.ngroups), dim3(64), lds, s.main, b.groups, b.f, b.fg);
-  BGV_MARK(5);
-  BGV_MARK(6);
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.ngroups, b.fg,
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups, b.f,
                      b.verdict);
-  BGV_MARK(7);
+  BGV_MARK(5);
   return hipGetLastError();
 }
 #undef BGV_MARK
@@ -479,7 +477,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
 size_t bgv_slot_bytes() {
   return sizeof(g2_aff) + sizeof(g2_jac) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
 }
-size_t bgv_group_bytes() { return sizeof(fp12_t) + sizeof(int32_t); }
+size_t bgv_group_bytes() { return sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
 
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
@@ -497,10 +495,8 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   b->sig_status = reinterpret_cast<int32_t*>(p);
   p += sizeof(int32_t) * (size_t)cap_slots;
   b->pk_status = reinterpret_cast<int32_t*>(p);
-  uint8_t* q = static_cast<uint8_t*>(group_mem);
-  b->fg = reinterpret_cast<fp12_t*>(q);
-  q += sizeof(fp12_t) * (size_t)cap_groups;
-  b->verdict = reinterpret_cast<int32_t*>(q);
+  (void)cap_groups;
+  b->verdict = static_cast<int32_t*>(group_mem);
 }
 
 hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_cache_entry* cache, int32_t* status,

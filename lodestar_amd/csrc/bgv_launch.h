@@ -34,17 +34,16 @@ struct bgv_dev_batch {
   fp12_t* f;          // per-slot 2-pair Miller loop value
   int32_t* sig_status;
   int32_t* pk_status;
-  fp12_t* fg;  // per-group product
-  int32_t* verdict;
+  int32_t* verdict;  // per group
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
 #endif
 };
 
 // kernels of one verify launch, in order (names for per-kernel timing)
-#define BGV_NKERNELS 4
+#define BGV_NKERNELS 3
 #define BGV_NSETKERNELS 2  // the first BGV_NSETKERNELS run once per call (bgv_launch_sets)
-static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_prep", "k_miller", "k_reduce", "k_final"};
+static const char* const BGV_KERNEL_NAMES[BGV_NKERNELS] = {"k_prep", "k_miller", "k_final"};
 struct bgv_streams {
   hipStream_t main;
   hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr

@@ -618,6 +618,31 @@ BGV_NOINLINE fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t&
   return fp12_t{c0, c1};
 }
 
+// f * l * l' for two lines l = (a0 + a1 v) + (b1 v) w, l' = (a0' + a1' v) + (b1' v) w
+// (fp12_mul_line's shape).  The lines are multiplied first (6 Fp2 products):
+//   l l' = (C0 + C1 v + C2 v^2) + (D1 v + D2 v^2) w
+//   C0 = a0 a0' + xi b1 b1',  C1 = a0 a1' + a1 a0',  C2 = a1 a1',
+//   D1 = a0 b1' + b1 a0',     D2 = a1 b1' + b1 a1'
+// (each cross sum by Karatsuba over the three diagonal products), then f times that
+// (t0 = f0 C, u = f1 (D1 + D2 v), f1 D = v u): 51 + 18 = 69 Fp products against 78
+// for two fp12_mul_line.
+BGV_NOINLINE fp12_t fp12_mul_lines(const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1,
+                                   const fp2_t& a0p, const fp2_t& a1p, const fp2_t& b1p) {
+  const fp2_t m00 = fp2_mul(a0, a0p), m11 = fp2_mul(a1, a1p), mbb = fp2_mul(b1, b1p);
+  fp6_t C;
+  C.c0 = fp2_add(m00, fp2_mul_xi(mbb));
+  C.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a0, a1), fp2_add_norm(a0p, a1p)), m00), m11);
+  C.c2 = m11;
+  const fp2_t D1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a0, b1), fp2_add_norm(a0p, b1p)), m00), mbb);
+  const fp2_t D2 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a1, b1), fp2_add_norm(a1p, b1p)), m11), mbb);
+  const fp6_t t0 = fp6_mul(f.c0, C);
+  const fp6_t t1 = fp6_mul_v(fp6_mul_01(f.c1, D1, D2));  // f1 D
+  const fp6_t CD = fp6_t{C.c0, fp2_add_norm(C.c1, D1), fp2_add_norm(C.c2, D2)};
+  const fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_norm(f.c0, f.c1), CD), t0), t1);
+  const fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
+  return fp12_t{c0, c1};
+}
+
 BGV_NOINLINE fp12_t fp12_inv(const fp12_t& a) {
   fp6_t n = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
   fp6_t ni = fp6_inv(n);

@@ -126,7 +126,7 @@ BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_af
   const fp_t xn1 = fp_neg(p1.x), xn2 = fp_neg(p2.x);
   const miller_jq c1 = miller_jq_make(q1, xn1, p1.y);
   g2_jac t1 = q1, t2 = jac_from_aff(q2);
-  fp2_t l0, l1, l3;
+  fp2_t l0, l1, l3, m0, m1, m3;
   const uint64_t X = BGV_X_ABS;
   miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
   fp12_t f = fp12_mul_line(fp12_one(), l0, l1, l3);
@@ -134,20 +134,24 @@ BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_af
     miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
     f = fp12_mul_line(f, l0, l1, l3);
   }
+  // both pairs' lines of a step are multiplied together before they meet f
+  // (fp12_mul_lines); a one-pair loop (infinity signature) takes them one by one
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
       miller_add_jq(t1, &l0, &l1, &l3, c1);
-      f = fp12_mul_line(f, l0, l1, l3);
       if (two) {
-        miller_add(t2, &l0, &l1, &l3, q2, xn2, p2.y);
+        miller_add(t2, &m0, &m1, &m3, q2, xn2, p2.y);
+        f = fp12_mul_lines(f, l0, l1, l3, m0, m1, m3);
+      } else {
         f = fp12_mul_line(f, l0, l1, l3);
       }
     }
     f = fp12_sqr(f);
     miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
-    f = fp12_mul_line(f, l0, l1, l3);
     if (two) {
-      miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
+      miller_dbl(t2, &m0, &m1, &m3, xn2, p2.y);
+      f = fp12_mul_lines(f, l0, l1, l3, m0, m1, m3);
+    } else {
       f = fp12_mul_line(f, l0, l1, l3);
     }
   }

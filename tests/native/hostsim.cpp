@@ -84,7 +84,12 @@ void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
   (void)miller_loop2(in_g1(p), jac_from_aff(in_g2(q)), g1_neg_generator(), in_g2(q), true);
 }
 void hs_k_final_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
-void hs_k_reduce_step(const uint8_t* f) { (void)fp12_mul(in_fp12(f), in_fp12(f)); }
+// one Fp12 product of the group product in k_final (operands already in Montgomery form)
+void hs_k_product_step(const uint8_t* f) {
+  const fp12_t a = in_fp12(f);
+  hs_count_reset();
+  (void)fp12_mul(a, a);
+}
 #endif
 
 void hs_fp_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) { out_fp(r, fp_mul(in_fp(a), in_fp(b))); }
@@ -117,6 +122,10 @@ void hs_fp12_frob2(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_frob2(in_fp1
 void hs_fp12_cyc_sqr(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_cyclotomic_sqr(in_fp12(a))); }
 void hs_fp12_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   out_fp12(r, fp12_mul_line(in_fp12(f), in_fp2(l0), in_fp2(l1), in_fp2(l3)));
+}
+void hs_fp12_mul_lines(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3,
+                       const uint8_t* m0, const uint8_t* m1, const uint8_t* m3) {
+  out_fp12(r, fp12_mul_lines(in_fp12(f), in_fp2(l0), in_fp2(l1), in_fp2(l3), in_fp2(m0), in_fp2(m1), in_fp2(m3)));
 }
 
 // G2 compressed (96 B) -> test-layout affine (192 B); returns BGV code, 100 = infinity

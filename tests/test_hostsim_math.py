@@ -116,6 +116,12 @@ def test_fp12_ops(L):
     line = (l0, o.F2_ZERO, l1, l3, o.F2_ZERO, o.F2_ZERO)
     L.hs_fp12_mul_line(r, f12_tower_bytes(a), hs.fp2_b(l0), hs.fp2_b(l1), hs.fp2_b(l3))
     assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_mul(a, line))
+    # two lines multiplied together first (miller_loop2's merged step)
+    m0, m1, m3 = rfp2(), rfp2(), rfp2()
+    line2 = (m0, o.F2_ZERO, m1, m3, o.F2_ZERO, o.F2_ZERO)
+    L.hs_fp12_mul_lines(r, f12_tower_bytes(a), hs.fp2_b(l0), hs.fp2_b(l1), hs.fp2_b(l3), hs.fp2_b(m0),
+                        hs.fp2_b(m1), hs.fp2_b(m3))
+    assert hs.b_fp12_tower(r.raw) == o.f12_to_tower_list(o.f12_mul(o.f12_mul(a, line), line2))
 
 
 def test_cyclotomic_sqr(L):

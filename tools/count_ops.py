@@ -55,9 +55,9 @@ def main():
     out["k_miller"] = list(count(lambda: L.hs_k_miller_body(hs.g1_b(pk), hs.g2_b(h))))
     f12 = hs.fp12_b_tower([rng.randrange(o.P) for _ in range(12)])
     out["k_final[per group]"] = list(count(lambda: L.hs_k_final_body(f12)))
-    out["k_reduce[per tree step]"] = list(count(lambda: L.hs_k_reduce_step(f12)))
+    out["k_final[per product step]"] = list(count(lambda: L.hs_k_product_step(f12)))
     res = {
-        "note": "Fp products [mul, sqr] per set (per group / per tree step where named), counted in the "
+        "note": "Fp products [mul, sqr] per set (per group / per group-product step where named), counted in the "
                 "kernels' own math (host build, -DBGV_COUNT_OPS). Fp-mul-eq = mul + sqr; "
                 "algorithmic u32 MACs per Fp-mul-eq = 288 (12x32-bit CIOS: 144 product + 144 reduction).",
         "macs_per_fp_mul": 288,
