@@ -83,9 +83,17 @@ BGV_HD jac_t<F> jac_neg(const jac_t<F>& p) {
   return jac_t<F>{p.x, f_neg(p.y), p.z};
 }
 
+// Jacobian doubling/addition: out of line by default; -DBGV_CURVE_INLINE inlines them
+// into their callers (the scalar-multiplication loops keep the point in VGPRs).
+#ifdef BGV_CURVE_INLINE
+#define BGV_CURVE_ATTR BGV_HD
+#else
+#define BGV_CURVE_ATTR BGV_NOINLINE
+#endif
+
 // dbl-2009-l
 template <class F>
-BGV_NOINLINE jac_t<F> jac_dbl(const jac_t<F>& p) {
+BGV_CURVE_ATTR jac_t<F> jac_dbl(const jac_t<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -125,7 +133,7 @@ BGV_HD jac_t<F> jac_add_raw(const jac_t<F>& p, const jac_t<F>& q, bool* h_zero, 
 
 // complete addition
 template <class F>
-BGV_NOINLINE jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
+BGV_CURVE_ATTR jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
   bool hz, rz;
   jac_t<F> r = jac_add_raw(p, q, &hz, &rz);
   const bool pinf = jac_is_inf(p), qinf = jac_is_inf(q);

@@ -42,6 +42,18 @@
 #define BGV_MUL_ATTR BGV_NOINLINE
 #endif
 
+// The tower functions of the Miller-loop step (fp6_mul, fp6_mul_01, fp12_sqr, the
+// line products, miller_dbl/add) are inlined into miller_loop2, so f, T and the
+// lines stay in VGPRs and only fp_mul/fp_sqr are calls: out of line, every
+// by-reference argument and struct return went through scratch, and at one wave
+// per SIMD nothing hid that latency (k_miller 51.4 -> 41.3 ms per 131,072 sets,
+// tools/gpu/variants.sh).  -DBGV_MILLER_OUTLINE restores the calls.
+#ifdef BGV_MILLER_OUTLINE
+#define BGV_MILLER_ATTR BGV_NOINLINE
+#else
+#define BGV_MILLER_ATTR BGV_HD
+#endif
+
 #define BGV_UNROLL _Pragma("unroll")
 #define BGV_NO_UNROLL _Pragma("unroll 1")
 
@@ -522,7 +534,7 @@ BGV_HD fp6_t fp6_mul_v(const fp6_t& a) { return fp6_t{fp2_mul_xi(a.c2), a.c0, a.
 
 // Operand coefficients: normalized, values < 4p (an fp6_add_norm of reduced values
 // at most); the result is weakly reduced.
-BGV_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
+BGV_MILLER_ATTR fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
   fp2_t t0 = fp2_mul(a.c0, b.c0);
   fp2_t t1 = fp2_mul(a.c1, b.c1);
   fp2_t t2 = fp2_mul(a.c2, b.c2);
@@ -550,7 +562,7 @@ BGV_NOINLINE fp6_t fp6_sqr(const fp6_t& a) {
 }
 
 // a * (b0 + b1 v)
-BGV_NOINLINE fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
+BGV_MILLER_ATTR fp6_t fp6_mul_01(const fp6_t& a, const fp2_t& b0, const fp2_t& b1) {
   fp2_t t0 = fp2_mul(a.c0, b0);
   fp2_t t1 = fp2_mul(a.c1, b1);
   fp2_t c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), t0);
@@ -601,7 +613,7 @@ BGV_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
   return fp12_t{c0, c1};
 }
 
-BGV_NOINLINE fp12_t fp12_sqr(const fp12_t& a) {
+BGV_MILLER_ATTR fp12_t fp12_sqr(const fp12_t& a) {
   fp6_t t = fp6_mul(a.c0, a.c1);
   fp6_t s = fp6_mul(fp6_add_norm(a.c0, a.c1), fp6_add_norm(a.c0, fp6_mul_v(a.c1)));
   fp6_t c0 = fp6_sub(fp6_sub(s, t), fp6_mul_v(t));
@@ -610,7 +622,7 @@ BGV_NOINLINE fp12_t fp12_sqr(const fp12_t& a) {
 
 // f * (l0 + l1 w^2 + l3 w^3): a line with nonzero tower coefficients
 // c0.c0 = l0, c0.c1 = l1, c1.c1 = l3.
-BGV_NOINLINE fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+BGV_MILLER_ATTR fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
   fp6_t t0 = fp6_mul_01(f.c0, l0, l1);
   fp6_t t1 = fp6_mul_1(f.c1, l3);
   fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add_norm(f.c0, f.c1), l0, fp2_add_norm(l1, l3)), t0), t1);
@@ -626,7 +638,7 @@ BGV_NOINLINE fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2_t&
 // (each cross sum by Karatsuba over the three diagonal products), then f times that
 // (t0 = f0 C, u = f1 (D1 + D2 v), f1 D = v u): 51 + 18 = 69 Fp products against 78
 // for two fp12_mul_line.
-BGV_NOINLINE fp12_t fp12_mul_lines(const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1,
+BGV_MILLER_ATTR fp12_t fp12_mul_lines(const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1,
                                    const fp2_t& a0p, const fp2_t& a1p, const fp2_t& b1p) {
   const fp2_t m00 = fp2_mul(a0, a0p), m11 = fp2_mul(a1, a1p), mbb = fp2_mul(b1, b1p);
   fp6_t C;
