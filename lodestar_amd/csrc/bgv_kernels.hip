@@ -181,7 +181,7 @@ struct tm_dev_ops {
   __device__ fp_t sqr(const fp_t& x) {
     if (c < BGV_TEAM_COMPS) A[c] = x;
     __syncthreads();
-    const fp_t r = tm_mul_lane(cc, A, A);
+    const fp_t r = tm_sqr_lane(cc, A);
     __syncthreads();
     return r;
   }

@@ -87,6 +87,52 @@ BGV_HD fp_t tm_mul_lane(int c, const fp_t* A, const fp_t* B) {
   return wide_redc(t);
 }
 
+// Coefficient c = 2k + e of a^2 with 7 double-width products instead of 12.  The
+// ordered pairs (i, j) and (j, i) of c_k = sum_{i+j = k (mod 6)} a_i a_j (xi-scaled when
+// i + j >= 6) carry the same product, so every lane takes 3 unordered pairs with the
+// generic two-product formula of tm_mul_lane, the x operand doubled for a cross pair
+// (i != j), plus, for even k, the unwrapped diagonal a_{k/2}^2 as one product:
+// re = (x0 + x1)(x0 - x1), im = (2 x0) x1.  Pairs per k (i, j, wrap):
+//   k=0: (1,5,w) (2,4,w) (3,3,w) + diag 0     k=1: (0,1) (2,5,w) (3,4,w)
+//   k=2: (0,2) (3,5,w) (4,4,w) + diag 1       k=3: (0,3) (1,2) (4,5,w)
+//   k=4: (0,4) (1,3) (5,5,w) + diag 2         k=5: (0,5) (1,4) (2,3)
+// Every lane runs the same 7 products (odd k multiplies zeros in the 7th), so a team
+// never diverges.  Bounds: operands < 4p, 7 products < 112 p^2, columns < 2^63.
+BGV_HD fp_t tm_sqr_lane(int c, const fp_t* A) {
+  const int k = c >> 1, e = c & 1;
+  // packed (i, j, wrap) per pair slot, indexed by k
+  const uint32_t kI[6] = {0x321, 0x320, 0x430, 0x410, 0x510, 0x210};
+  const uint32_t kJ[6] = {0x345, 0x451, 0x452, 0x523, 0x534, 0x345};
+  const uint32_t kW[6] = {0x7, 0x6, 0x6, 0x4, 0x4, 0x0};
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int q = 0; q < 2 * NL; ++q) t[q] = 0;
+  BGV_NO_UNROLL for (int p = 0; p < 3; ++p) {
+    const int i = (kI[k] >> (4 * p)) & 0xf, j = (kJ[k] >> (4 * p)) & 0xf;
+    const bool wrap = (kW[k] >> p) & 1;
+    const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+    const fp_t y0 = A[2 * j], y1 = A[2 * j + 1];
+    const fp_t d = fp_sub_nr(y0, y1);
+    const fp_t s = fp_add_norm(y0, y1);
+    const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+    const fp_t X2n = fp_select(e != 0, x1n, x1);
+    const bool cross = i != j;  // a cross pair is counted twice
+    const fp_t X1 = fp_select(cross, x0, fp_add_norm(x0, x0));
+    const fp_t X2 = fp_select(cross, X2n, fp_add_norm(X2n, X2n));
+    const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+    const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+    wide_mac(t, X1, Y1);
+    wide_mac(t, X2, Y2);
+  }
+  // unwrapped diagonal (even k): re (x0 + x1)(x0 - x1 + 2p), im (2 x0) x1; odd k adds 0
+  const int h = k >> 1;
+  const fp_t x0 = A[2 * h], x1 = A[2 * h + 1];
+  const bool even = (k & 1) == 0;
+  const fp_t P = e ? fp_add_norm(x0, x0) : fp_add_norm(x0, x1);
+  const fp_t Q = e ? x1 : fp_sub_nr(x0, x1);
+  wide_mac(t, fp_select(even, fp_zero(), P), Q);
+  return wide_redc(t);
+}
+
 // Frobenius (p-power) on the component pair (x0, x1) = f_k:
 // frob(f)_k = conj(f_k) * g_k, g = BGV_FROB1 indexed by tower position.
 BGV_HD fp_t tm_frob_lane(int c, const fp_t& x0, const fp_t& x1, const fp2_t& g) {
@@ -141,7 +187,11 @@ struct tm_emu_ops {
     for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_mul_lane(c, a.c, b.c);
     return r;
   }
-  BGV_HD tm_emu_t sqr(const tm_emu_t& a) { return mul(a, a); }
+  BGV_HD tm_emu_t sqr(const tm_emu_t& a) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_sqr_lane(c, a.c);
+    return r;
+  }
   BGV_HD tm_emu_t conj(const tm_emu_t& a) {
     tm_emu_t r = a;
     for (int c = 0; c < BGV_TEAM_COMPS; ++c)

@@ -10,6 +10,12 @@
  *
  * Pubkeys are validator indices into the device-resident cache (SURVEY §7 "pubkey identity at
  * the boundary", option (a)): set.pubkey / set.pubkeys hold numbers (or {index}).
+ *
+ * Metrics: with modules.metrics (the beacon node's IMetrics) the verifier feeds the same
+ * bls / blsThreadPool series as the pool (metrics/metrics/lodestar.ts:405-494, updated at
+ * multithread/index.ts:129-130,136-151,317-367); the whole device is worker 0, and the
+ * per-call device time stands in for the worker job time.  latencyToWorker/FromWorker
+ * (structured-clone messaging) have no GPU counterpart and are not observed.
  */
 const path = require("path");
 const addon = require(path.join(__dirname, "blsgpu.node"));
@@ -80,14 +86,25 @@ class BlsGpuVerifier {
     this.bufferedJobs = null;
     this.closed = false;
     this.counters = {aggregatedPubkeys: 0, batchRetries: 0, successJobsSignatureSetsCount: 0, errorJobsSignatureSetsCount: 0};
+    const metrics = this.metrics;
+    if (metrics) {
+      metrics.blsThreadPool.queueLength.addCollect(() => metrics.blsThreadPool.queueLength.set(this.jobs.length));
+    }
   }
 
   async verifySignatureSets(sets, opts = {}) {
-    this.counters.aggregatedPubkeys += getAggregatedPubkeysCount(sets);
+    const nAgg = getAggregatedPubkeysCount(sets);
+    this.counters.aggregatedPubkeys += nAgg;
+    if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(nAgg);
     if (opts.verifyOnMainThread && !this.blsVerifyAllMultiThread) {
       // index.ts:138-151: one job verified at once (no buffering)
-      const codes = await addon.verify(this.ctx, [{sets: sets.map(toNativeSet), batchable: false}], 1);
-      return unwrap(codes[0]);
+      const timer = this.metrics ? this.metrics.blsThreadPool.mainThreadDurationInThreadPool.startTimer() : null;
+      try {
+        const codes = await addon.verify(this.ctx, [{sets: sets.map(toNativeSet), batchable: false}], 1);
+        return unwrap(codes[0]);
+      } finally {
+        if (timer) timer();
+      }
     }
     const results = await Promise.all(
       chunkifyMaximizeChunkSize(sets, MAX_SIGNATURE_SETS_PER_JOB).map((chunk) =>
@@ -111,7 +128,7 @@ class BlsGpuVerifier {
   queueBlsWork(workReq) {
     if (this.closed) return Promise.reject(new QueueError("QUEUE_ABORTED"));
     return new Promise((resolve, reject) => {
-      const job = {resolve, reject, workReq};
+      const job = {resolve, reject, workReq, addedTimeMs: Date.now()};
       if (workReq.opts.batchable) {
         if (!this.bufferedJobs) {
           this.bufferedJobs = {jobs: [], sigCount: 0, timeout: setTimeout(this.runBufferedJobs, this.maxBufferWaitMs)};
@@ -142,22 +159,48 @@ class BlsGpuVerifier {
   runJob = async () => {
     if (this.closed || this.jobs.length === 0) return;
     const jobs = this.jobs.splice(0, this.jobs.length);
+    const m = this.metrics ? this.metrics.blsThreadPool : null;
+    let startedSigSets = 0;
+    for (const job of jobs) {
+      startedSigSets += job.workReq.sets.length;
+      if (m) m.jobWaitTime.observe((Date.now() - job.addedTimeMs) / 1000);
+    }
+    if (m) {
+      m.totalJobsGroupsStarted.inc(1);
+      m.totalJobsStarted.inc(jobs.length);
+      m.totalSigSetsStarted.inc(startedSigSets);
+    }
     try {
       const codes = await addon.verify(
         this.ctx,
         jobs.map((j) => ({sets: j.workReq.sets, batchable: Boolean(j.workReq.opts.batchable)})),
         0
       );
+      let successCount = 0;
+      let errorCount = 0;
       jobs.forEach((job, i) => {
         const c = codes[i];
         if (c < 0) {
-          this.counters.errorJobsSignatureSetsCount += job.workReq.sets.length;
+          errorCount += job.workReq.sets.length;
           job.reject(Error(addon.strerror(-c)));
         } else {
-          this.counters.successJobsSignatureSetsCount += job.workReq.sets.length;
+          successCount += job.workReq.sets.length;
           job.resolve(c === 1);
         }
       });
+      const st = codes.stats || {batchRetries: 0, batchSigsSuccess: 0, deviceMs: 0};
+      this.counters.successJobsSignatureSetsCount += successCount;
+      this.counters.errorJobsSignatureSetsCount += errorCount;
+      this.counters.batchRetries += st.batchRetries;
+      if (m) {
+        const jobTimeSec = st.deviceMs / 1000;
+        m.timePerSigSet.observe(jobTimeSec / Math.max(1, startedSigSets));
+        m.jobsWorkerTime.inc({workerId: 0}, jobTimeSec);
+        m.successJobsSignatureSetsCount.inc(successCount);
+        m.errorJobsSignatureSetsCount.inc(errorCount);
+        m.batchRetries.inc(st.batchRetries);
+        m.batchSigsSuccess.inc(st.batchSigsSuccess);
+      }
     } catch (e) {
       for (const job of jobs) job.reject(e);
     }

@@ -167,6 +167,7 @@ typedef struct {
   size_t nsets;
   int mode;
   int32_t* codes;
+  bgv_stats stats;
   int rc;
   napi_deferred deferred;
   napi_async_work work;
@@ -177,7 +178,7 @@ typedef struct {
 static void verify_execute(napi_env env, void* data) {
   (void)env;
   verify_req* r = (verify_req*)data;
-  r->rc = bgv_verify(r->ctx, r->jobs, r->njobs, r->sets, r->nsets, r->mode, r->codes, NULL);
+  r->rc = bgv_verify(r->ctx, r->jobs, r->njobs, r->sets, r->nsets, r->mode, r->codes, &r->stats);
 }
 
 static void verify_complete(napi_env env, napi_status status, void* data) {
@@ -193,6 +194,22 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
     napi_create_arraybuffer(env, 4 * r->njobs, &dst, &ab);
     memcpy(dst, r->codes, 4 * r->njobs);
     napi_create_typedarray(env, napi_int32_array, r->njobs, ab, 0, &arr);
+    /* codes.stats: the call's BlsWorkResult-style counters (multithread/types.ts:24-36) */
+    napi_value st, v;
+    napi_create_object(env, &st);
+    napi_create_double(env, (double)r->stats.batch_retries, &v);
+    napi_set_named_property(env, st, "batchRetries", v);
+    napi_create_double(env, (double)r->stats.batch_sigs_success, &v);
+    napi_set_named_property(env, st, "batchSigsSuccess", v);
+    napi_create_double(env, (double)r->stats.device_groups, &v);
+    napi_set_named_property(env, st, "deviceGroups", v);
+    napi_create_double(env, (double)r->stats.sets_verified, &v);
+    napi_set_named_property(env, st, "setsVerified", v);
+    napi_create_double(env, r->stats.device_ms, &v);
+    napi_set_named_property(env, st, "deviceMs", v);
+    napi_create_double(env, r->stats.wall_ms, &v);
+    napi_set_named_property(env, st, "wallMs", v);
+    napi_set_named_property(env, arr, "stats", st);
     napi_resolve_deferred(env, r->deferred, arr);
   }
   for (size_t i = 0; i < r->nrefs; ++i) napi_delete_reference(env, r->refs[i]);

@@ -216,6 +216,10 @@ void hs_team_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {
   tm_emu_ops o;
   out_fp12(r, tm_emu_to_fp12(o.mul(tm_emu_from_fp12(in_fp12(a)), tm_emu_from_fp12(in_fp12(b)))));
 }
+void hs_team_sqr(uint8_t* r, const uint8_t* a) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.sqr(tm_emu_from_fp12(in_fp12(a)))));
+}
 void hs_team_frob(uint8_t* r, const uint8_t* a) {
   tm_emu_ops o;
   out_fp12(r, tm_emu_to_fp12(o.frob(tm_emu_from_fp12(in_fp12(a)))));

@@ -119,6 +119,53 @@ async function gpuChecks() {
   assert.strictEqual(await pool.verifySignatureSets(gswap, {batchable: true}), false);
   report.goldenBytes = "ok";
 
+  // metrics parity: the pool's bls / blsThreadPool series (metrics/lodestar.ts:405-494)
+  const rec = {};
+  const series = (name) => {
+    rec[name] = {n: 0, sum: 0, labels: []};
+    return {
+      inc: (a, b) => {
+        const v = typeof a === "object" ? b : a === undefined ? 1 : a;
+        if (typeof a === "object") rec[name].labels.push(a);
+        rec[name].n++;
+        rec[name].sum += v;
+      },
+      observe: (v) => {
+        rec[name].n++;
+        rec[name].sum += v;
+      },
+      set: (v) => (rec[name].sum = v),
+      addCollect: (fn) => (rec[name].collect = fn),
+      startTimer: () => () => rec[name].n++,
+    };
+  };
+  const names = ["queueLength", "mainThreadDurationInThreadPool", "jobWaitTime", "totalJobsGroupsStarted",
+    "totalJobsStarted", "totalSigSetsStarted", "timePerSigSet", "jobsWorkerTime", "successJobsSignatureSetsCount",
+    "errorJobsSignatureSetsCount", "batchRetries", "batchSigsSuccess"];
+  const metrics = {bls: {aggregatedPubkeys: series("aggregatedPubkeys")}, blsThreadPool: {}};
+  for (const n of names) metrics.blsThreadPool[n] = series(n);
+  const mpool = new BlsGpuVerifier({maxBufferWaitMs: 20, ctx: pool.ctx}, {metrics});
+  const mres = await Promise.all([
+    mpool.verifySignatureSets(sets, {batchable: true}),
+    mpool.verifySignatureSets([wrong], {batchable: true}),
+    mpool.verifySignatureSets([aggSet], {batchable: true}),
+    mpool.verifySignatureSets([invalidSet], {batchable: true}).catch((e) => e.message),
+  ]);
+  assert.deepStrictEqual(mres, [true, false, true, "BLST_INVALID_SIZE"]);
+  assert.strictEqual(await mpool.verifySignatureSets(sets, {verifyOnMainThread: true}), true);
+  const tp = (n) => rec[n];
+  assert.strictEqual(rec.aggregatedPubkeys.sum, 3);
+  assert.strictEqual(tp("totalJobsStarted").sum, 4);
+  assert.strictEqual(tp("totalSigSetsStarted").sum, N + 3);
+  assert.strictEqual(tp("jobWaitTime").n, 4);
+  assert.strictEqual(tp("successJobsSignatureSetsCount").sum, N + 2);
+  assert.strictEqual(tp("errorJobsSignatureSetsCount").sum, 1);
+  assert.ok(tp("batchRetries").sum >= 1, "the mixed batch was retried");
+  assert.ok(tp("jobsWorkerTime").sum > 0 && tp("jobsWorkerTime").labels[0].workerId === 0);
+  assert.strictEqual(tp("mainThreadDurationInThreadPool").n, 1);
+  assert.strictEqual(typeof tp("queueLength").collect, "function");
+  report.metrics = "ok";
+
   // close(): queued work rejects with QUEUE_ABORTED, later calls too (index.ts:176-197,239-241)
   const pending = pool.verifySignatureSets(sets, {batchable: true});
   await pool.close();

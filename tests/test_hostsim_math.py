@@ -304,6 +304,9 @@ def test_team_fp12_ops(L):
         L.hs_fp12_mul(want, a, b)
         L.hs_team_mul(got, a, b)
         assert got.raw == want.raw
+        L.hs_fp12_sqr(want, a)
+        L.hs_team_sqr(got, a)  # 7-product team squaring
+        assert got.raw == want.raw
         for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
             tf(got, a)
             ref(want, a)
