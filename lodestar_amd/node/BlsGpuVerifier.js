@@ -205,6 +205,50 @@ class BlsGpuVerifier {
       for (const job of jobs) job.reject(e);
     }
   };
+
+  // ---- SURVEY 8(f) entry points (synchronous; low volume beside verifySignatureSets) ----
+
+  /** bls.Signature.aggregate(sigs.map((s) => Signature.fromBytes(s, undefined, true))).toBytes()
+   * (chain/opPools/attestationPool.ts:184-187): throws Error(BLST code) like the dependency. */
+  aggregateSignatures(sigs) {
+    return this.aggregateSignaturesMany([sigs])[0];
+  }
+
+  /** One aggregate per op-pool entry in a single device call; each element is the compressed
+   * aggregate or an Error carrying the BLST code of its first failing signature. */
+  aggregateSignaturesMany(aggregates) {
+    const {status, sigs} = addon.aggregateSignatures(this.ctx, aggregates);
+    return aggregates.map((_, a) => {
+      if (status[a] < 0) throw Error(addon.strerror(-status[a]));
+      return sigs.slice(96 * a, 96 * a + 96);
+    });
+  }
+
+  /** Deposit-time key check, PublicKey.fromBytes(pk, affine, true) (processDeposit.ts:64):
+   * per key null (valid) or the BLST code name. */
+  validatePubkeys(keys48) {
+    const flat = new Uint8Array(48 * keys48.length);
+    keys48.forEach((k, i) => {
+      if (k.length !== 48) throw Error("BLST_BAD_ENCODING");
+      flat.set(k, 48 * i);
+    });
+    const {status} = addon.pubkeysValidate(this.ctx, flat);
+    return Array.from(status, (c) => (c === 0 ? null : addon.strerror(-c)));
+  }
+
+  /** processDeposit.ts:62-70 signature check over {pubkey, signingRoot, signature} records. */
+  verifyDeposits(deposits) {
+    const n = deposits.length;
+    const keys = new Uint8Array(48 * n);
+    const roots = new Uint8Array(32 * n);
+    const sigs = new Uint8Array(96 * n);
+    deposits.forEach((d, i) => {
+      keys.set(d.pubkey, 48 * i);
+      roots.set(d.signingRoot, 32 * i);
+      sigs.set(d.signature, 96 * i);
+    });
+    return Array.from(addon.depositsVerify(this.ctx, keys, roots, sigs), (v) => v === 1);
+  }
 }
 
 function unwrap(code) {

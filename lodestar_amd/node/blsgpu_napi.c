@@ -15,6 +15,12 @@
  *          mode: 0 | 1) -> Promise<Int32Array>   (1 valid, 0 invalid, -code error)
  *   strerror(code) -> string
  *   close(ctx)
+ * SURVEY 8(f) entry points and parity hooks (synchronous):
+ *   aggregatePubkeys(ctx, indices: Uint32Array) -> Uint8Array (96-B uncompressed)
+ *   hashToG2(ctx, msg: Uint8Array) -> Uint8Array (192-B uncompressed)
+ *   pubkeysValidate(ctx, keys48) -> {status: Int32Array, uncompressed: Uint8Array}
+ *   aggregateSignatures(ctx, aggregates: Uint8Array[][]) -> {status: Int32Array, sigs: Uint8Array}
+ *   depositsVerify(ctx, keys48, msgs32, sigs96) -> Int32Array (1 | 0)
  */
 #include <node_api.h>
 #include <stdlib.h>
@@ -155,6 +161,172 @@ static napi_value js_sign(napi_env env, napi_callback_info info) {
   int rc = bgv_sign(ctx, sks, msgs, l1 / 32, (uint8_t*)dst);
   if (rc) return throw_code(env, rc);
   CHECK(env, napi_create_typedarray(env, napi_uint8_array, 96 * (l1 / 32), ab, 0, &out));
+  return out;
+}
+
+/* ---- SURVEY 8(f) entry points and parity hooks (synchronous: low volume) ---- */
+
+static napi_value new_bytes(napi_env env, size_t n, void** dst) {
+  napi_value ab, out;
+  if (napi_create_arraybuffer(env, n, dst, &ab) != napi_ok) return NULL;
+  if (napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &out) != napi_ok) return NULL;
+  return out;
+}
+
+static napi_value new_int32s(napi_env env, const int32_t* src, size_t n) {
+  napi_value ab, out;
+  void* dst;
+  if (napi_create_arraybuffer(env, 4 * n, &dst, &ab) != napi_ok) return NULL;
+  if (n) memcpy(dst, src, 4 * n);
+  if (napi_create_typedarray(env, napi_int32_array, n, ab, 0, &out) != napi_ok) return NULL;
+  return out;
+}
+
+/* aggregatePubkeys(ctx, indices: Uint32Array) -> Uint8Array(96): PublicKey.aggregate +
+ * toBytes(uncompressed) over cached keys (chain/bls/utils.ts:5-16). */
+static napi_value js_aggregate_pubkeys(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t* idx;
+  size_t len;
+  if (get_bytes(env, argv[1], &idx, &len) || len % 4) return throw_code(env, -BGV_E_ARG);
+  void* dst;
+  napi_value out = new_bytes(env, 96, &dst);
+  if (!out) return throw_code(env, -BGV_E_ARG);
+  int rc = bgv_aggregate_pubkeys(ctx, (const uint32_t*)idx, len / 4, (uint8_t*)dst);
+  if (rc) return throw_code(env, rc);
+  return out;
+}
+
+/* hashToG2(ctx, msg: Uint8Array) -> Uint8Array(192) uncompressed (x.c1|x.c0|y.c1|y.c0) */
+static napi_value js_hash_to_g2(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t* msg;
+  size_t len;
+  if (get_bytes(env, argv[1], &msg, &len)) return throw_code(env, -BGV_E_ARG);
+  uint32_t l32 = (uint32_t)len;
+  void* dst;
+  napi_value out = new_bytes(env, 192, &dst);
+  if (!out) return throw_code(env, -BGV_E_ARG);
+  int rc = bgv_hash_to_g2(ctx, msg, &l32, 1, (uint8_t*)dst);
+  if (rc) return throw_code(env, rc);
+  return out;
+}
+
+/* pubkeysValidate(ctx, keys48: Uint8Array (n x 48)) -> {status: Int32Array (0 | -BLST code),
+ * uncompressed: Uint8Array (n x 96)}: PublicKey.fromBytes(pk, affine, validate=true) per key
+ * (state-transition/src/block/processDeposit.ts:64). */
+static napi_value js_pubkeys_validate(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t* keys;
+  size_t len;
+  if (get_bytes(env, argv[1], &keys, &len) || len % 48) return throw_code(env, -BGV_E_ARG);
+  const size_t n = len / 48;
+  int32_t* st = (int32_t*)calloc(n ? n : 1, sizeof(int32_t));
+  void* dst;
+  napi_value recs = new_bytes(env, 96 * n, &dst);
+  if (!recs) {
+    free(st);
+    return throw_code(env, -BGV_E_ARG);
+  }
+  int rc = bgv_pubkeys_validate(ctx, keys, n, st, (uint8_t*)dst);
+  if (rc) {
+    free(st);
+    return throw_code(env, rc);
+  }
+  napi_value out, status = new_int32s(env, st, n);
+  free(st);
+  CHECK(env, napi_create_object(env, &out));
+  CHECK(env, napi_set_named_property(env, out, "status", status));
+  CHECK(env, napi_set_named_property(env, out, "uncompressed", recs));
+  return out;
+}
+
+/* aggregateSignatures(ctx, aggregates: Uint8Array[][]) -> {status: Int32Array, sigs: Uint8Array
+ * (naggs x 96 compressed)}: Signature.aggregate over validated signatures, one entry per
+ * op-pool aggregate (chain/opPools/attestationPool.ts:184-187 and siblings). */
+static napi_value js_aggregate_signatures(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint32_t naggs = 0;
+  if (napi_get_array_length(env, argv[1], &naggs) != napi_ok) return throw_code(env, -BGV_E_ARG);
+  uint32_t* counts = (uint32_t*)calloc(naggs ? naggs : 1, sizeof(uint32_t));
+  size_t total = 0;
+  for (uint32_t a = 0; a < naggs; ++a) {
+    napi_value agg;
+    napi_get_element(env, argv[1], a, &agg);
+    if (napi_get_array_length(env, agg, &counts[a]) != napi_ok) {
+      free(counts);
+      return throw_code(env, -BGV_E_ARG);
+    }
+    total += counts[a];
+  }
+  /* records are zero-padded to 96 B; lens carries the received size (BLST_INVALID_SIZE) */
+  uint8_t* raw = (uint8_t*)calloc(total ? total : 1, 96);
+  uint32_t* lens = (uint32_t*)calloc(total ? total : 1, sizeof(uint32_t));
+  int32_t* st = (int32_t*)calloc(naggs ? naggs : 1, sizeof(int32_t));
+  size_t k = 0;
+  int bad = 0;
+  for (uint32_t a = 0; a < naggs && !bad; ++a) {
+    napi_value agg;
+    napi_get_element(env, argv[1], a, &agg);
+    for (uint32_t i = 0; i < counts[a]; ++i, ++k) {
+      napi_value s;
+      uint8_t* d;
+      size_t l;
+      napi_get_element(env, agg, i, &s);
+      if (get_bytes(env, s, &d, &l)) {
+        bad = 1;
+        break;
+      }
+      memcpy(raw + 96 * k, d, l < 96 ? l : 96);
+      lens[k] = (uint32_t)l;
+    }
+  }
+  void* dst;
+  napi_value sigs = bad ? NULL : new_bytes(env, 96 * (size_t)naggs, &dst);
+  int rc = sigs ? bgv_aggregate_signatures(ctx, raw, lens, counts, naggs, (uint8_t*)dst, st) : -BGV_E_ARG;
+  napi_value status = rc ? NULL : new_int32s(env, st, naggs);
+  free(raw);
+  free(lens);
+  free(counts);
+  free(st);
+  if (rc) return throw_code(env, rc);
+  napi_value out;
+  CHECK(env, napi_create_object(env, &out));
+  CHECK(env, napi_set_named_property(env, out, "status", status));
+  CHECK(env, napi_set_named_property(env, out, "sigs", sigs));
+  return out;
+}
+
+/* depositsVerify(ctx, keys48, msgs32, sigs96) -> Int32Array (1 valid, 0 invalid): the
+ * deposit signature check of processDeposit.ts:62-70. */
+static napi_value js_deposits_verify(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  uint8_t *keys, *msgs, *sigs;
+  size_t lk, lm, ls;
+  if (get_bytes(env, argv[1], &keys, &lk) || get_bytes(env, argv[2], &msgs, &lm) ||
+      get_bytes(env, argv[3], &sigs, &ls) || lk % 48 || lm != 32 * (lk / 48) || ls != 96 * (lk / 48))
+    return throw_code(env, -BGV_E_ARG);
+  const size_t n = lk / 48;
+  int32_t* valid = (int32_t*)calloc(n ? n : 1, sizeof(int32_t));
+  int rc = bgv_deposits_verify(ctx, keys, msgs, sigs, n, valid);
+  napi_value out = rc ? NULL : new_int32s(env, valid, n);
+  free(valid);
+  if (rc) return throw_code(env, rc);
   return out;
 }
 
@@ -316,6 +488,11 @@ static napi_value init_module(napi_env env, napi_value exports) {
       {"keygen", NULL, js_keygen, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"sign", NULL, js_sign, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"verify", NULL, js_verify, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"aggregatePubkeys", NULL, js_aggregate_pubkeys, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"hashToG2", NULL, js_hash_to_g2, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"pubkeysValidate", NULL, js_pubkeys_validate, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"aggregateSignatures", NULL, js_aggregate_signatures, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"depositsVerify", NULL, js_deposits_verify, NULL, NULL, NULL, METHOD_ATTR, NULL},
   };
   napi_define_properties(env, exports, sizeof(d) / sizeof(d[0]), d);
   napi_value n;

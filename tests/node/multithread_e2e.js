@@ -9,7 +9,8 @@ const {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, 
 );
 
 function cpuChecks() {
-  for (const f of ["init", "close", "strerror", "pubkeysPut", "keygen", "sign", "verify"]) {
+  for (const f of ["init", "close", "strerror", "pubkeysPut", "keygen", "sign", "verify", "aggregatePubkeys",
+    "hashToG2", "pubkeysValidate", "aggregateSignatures", "depositsVerify"]) {
     assert.strictEqual(typeof addon[f], "function", f);
   }
   assert.strictEqual(addon.strerror(8), "BLST_INVALID_SIZE");
@@ -118,6 +119,38 @@ async function gpuChecks() {
   const gswap = [Object.assign({}, gsets[0], {signature: gsets[1].signature})];
   assert.strictEqual(await pool.verifySignatureSets(gswap, {batchable: true}), false);
   report.goldenBytes = "ok";
+
+  // parity hooks through the addon: PublicKey.aggregate (utils.ts:5-16) and hash_to_G2 bytes.
+  // Interop keys are appended at cache indices N.. (the cache has no holes), after the keygen keys.
+  const K0 = N;
+  const pkRec = new Uint8Array(96 * keys.pk_uncompressed.length);
+  keys.pk_uncompressed.forEach((h, i) => pkRec.set(hex(h), 96 * i));
+  addon.pubkeysPut(pool.ctx, K0, pkRec, 96);
+  for (const c of gold("aggregates.json").cases) {
+    const idx = Uint32Array.from(c.indices, (i) => i + K0);
+    assert.strictEqual(Buffer.from(addon.aggregatePubkeys(pool.ctx, idx)).toString("hex"), c.uncompressed);
+  }
+  for (const c of gold("hash_to_g2.json").cases.slice(0, 8)) {
+    assert.strictEqual(Buffer.from(addon.hashToG2(pool.ctx, hex(c.msg))).toString("hex"), c.uncompressed);
+  }
+  report.parityHooks = "ok";
+
+  // SURVEY 8(f): deposit key validation, op-pool signature aggregation, deposit signatures
+  // against tests/golden/next.json (codes are BLST numbers; 0 = valid)
+  const next = gold("next.json");
+  const codeName = (c) => (c === 0 ? null : addon.strerror(c));
+  assert.deepStrictEqual(pool.validatePubkeys(next.pubkeys.map((c) => hex(c.pk))), next.pubkeys.map((c) => codeName(c.expect)));
+  for (const c of next.aggregates) {
+    const sigs = c.sigs.map(hex);
+    if (c.expect === 0) {
+      assert.strictEqual(Buffer.from(pool.aggregateSignatures(sigs)).toString("hex"), c.aggregate);
+    } else {
+      assert.throws(() => pool.aggregateSignatures(sigs), (e) => e.message === addon.strerror(c.expect));
+    }
+  }
+  const deps = next.deposits.map((c) => ({pubkey: hex(c.pk), signingRoot: hex(c.msg), signature: hex(c.sig)}));
+  assert.deepStrictEqual(pool.verifyDeposits(deps), next.deposits.map((c) => c.expect === 1));
+  report.next = "ok";
 
   // metrics parity: the pool's bls / blsThreadPool series (metrics/lodestar.ts:405-494)
   const rec = {};

@@ -35,5 +35,6 @@ def test_addon_loads_and_exports():
 @pytest.mark.gpu
 def test_node_verifier_e2e():
     out = _run([], 110)
-    for k in ("sync", "async", "batched", "firstInvalid", "wrongSig", "aggregate", "chunked", "goldenBytes", "metrics", "close"):
+    for k in ("sync", "async", "batched", "firstInvalid", "wrongSig", "aggregate", "chunked", "goldenBytes", "parityHooks", "next", "metrics",
+              "close"):
         assert out[k] == "ok", out
