@@ -32,7 +32,10 @@ def build(force=False, verbose=True, lib=LIB, defines=()):
     if not force and up_to_date(lib):
         return lib
     objs = []
-    for src in SOURCES:
+    srcs = list(SOURCES)
+    if "BGV_MILLER_SPLIT" in defines:  # k_miller in its own unit, Fp products inlined
+        srcs.insert(1, os.path.join(CSRC, "bgv_kernels_miller.hip"))
+    for src in srcs:
         obj = os.path.join(CSRC, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
                "-c", src, "-o", obj] + ["-D" + d for d in defines]

@@ -29,7 +29,9 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BGV_HD __host__ __device__ __forceinline__
+#ifndef BGV_NOINLINE  // bgv_kernels_miller.hip makes its copies static (one TU per kernel set)
 #define BGV_NOINLINE __host__ __device__ __noinline__
+#endif
 #else
 #define BGV_HD inline __attribute__((always_inline))
 #define BGV_NOINLINE __attribute__((noinline))

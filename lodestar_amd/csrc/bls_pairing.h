@@ -122,7 +122,10 @@ BGV_MILLER_ATTR void miller_add_jq(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, c
 // f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) (conjugated) with one shared accumulator: the
 // squarings of f are paid once for both pairs.  two == false drops the second pair.
 // Q1 (= H(m)) is Jacobian: its additions use miller_add_jq, saving the inversion.
-BGV_NOINLINE fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
+#ifndef BGV_MILLER_LOOP_ATTR  // bgv_kernels_miller.hip inlines the loop into k_miller
+#define BGV_MILLER_LOOP_ATTR BGV_NOINLINE
+#endif
+BGV_MILLER_LOOP_ATTR fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
   const fp_t xn1 = fp_neg(p1.x), xn2 = fp_neg(p2.x);
   const miller_jq c1 = miller_jq_make(q1, xn1, p1.y);
   g2_jac t1 = q1, t2 = jac_from_aff(q2);
