@@ -1,6 +1,6 @@
 """Benchmark: verified signature sets/sec at 8192-set batches (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gossip8192|agg1024|block|...]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--inflight B] [--no-cpu-baseline] [--no-block-import]
 
 A step = one pass of the hot path over one synthetic batch: bgv_verify of 8192
 signature sets (config 4: gossip shape, 8192 batchable one-set jobs, 1 %
@@ -17,6 +17,9 @@ The JSON line carries:
                against the gfx950 peak v_mad_u64_u32 rate (16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz)
   cpu_baseline the C++ CPU restatement (oracle/cpu, worker-pool policy, up to 16 threads) on a
                bounded sample of the same batch
+  block_import config 3 of BASELINE.json, measured after the timed region: p50 latency of one
+               non-batchable 131-set call (randao + 128 attestations x 128 keys + 512-key sync
+               aggregate + proposer), one call at a time
 """
 import argparse
 import hashlib
@@ -110,6 +113,50 @@ def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0
     return jobs, expect, key_of
 
 
+def make_block_import(ctx, native, nkeys):
+    """config 3: one non-batchable call of 131 sets as chain/blocks/
+    verifyBlocksSignatures.ts:34 sends it: randao (single), 128 aggregate attestations of
+    128 distinct validators each, one sync-committee aggregate of 512 validators, and the
+    proposer signature (single).  Aggregate signatures sign with the summed secret key, so
+    every set is valid; pubkeys are aggregated on the device from the cache."""
+    sk_int = lambda i: int.from_bytes(interop_sk(i), "big")
+    root = lambda tag, i: hashlib.sha256(b"lodestar-block" + tag + i.to_bytes(4, "little")).digest()
+    groups = [("randao", [0])] + [("att", list(range(128 * a, 128 * a + 128))) for a in range(128)]
+    groups += [("sync", list(range(16384, 16384 + 512))), ("proposer", [1])]
+    assert max(max(k) for _, k in groups) < nkeys, "block import needs >= 16896 cached keys"
+    msgs = [root(tag.encode(), i) for i, (tag, _) in enumerate(groups)]
+    sks = [(sum(sk_int(k) for k in keys) % R_ORDER).to_bytes(32, "big") for _, keys in groups]
+    sigs = ctx.sign(b"".join(sks), b"".join(msgs))
+    sets = [native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=keys) for i, (_, keys) in enumerate(groups)]
+    return [(sets, False)]
+
+
+def block_import_latency(ctx, native, nkeys, runs=100):
+    jobs = make_block_import(ctx, native, nkeys)
+    packed = native.PackedCall(jobs)  # set records packed once, as the N-API addon hands them over
+    out = (native.ctypes.c_int32 * 1)()
+
+    def call():
+        rc = ctx.lib.bgv_verify(ctx.handle, packed.jobs, 1, packed.sets, packed.nsets, native.MODE_WORKER, out, None)
+        if rc != 0:
+            raise native.DeviceError(native.strerror(rc))
+        return out[0]
+
+    for _ in range(3):
+        assert call() == 1, "block import verdict mismatch"
+    lat = []
+    for _ in range(runs):
+        ts = time.perf_counter()
+        got = call()
+        lat.append(time.perf_counter() - ts)
+        assert got == 1, "block import verdict mismatch"
+    n_pk = sum(len(s.pk_indices) for s in jobs[0][0])
+    return {"config": "config3: 1 non-batchable call, 131 sets (randao + 128 x 128-key attestations + 512-key sync "
+                      "aggregate + proposer), %d pubkeys aggregated on the device" % n_pk,
+            "p50_latency_ms": 1e3 * statistics.median(lat), "p90_latency_ms": 1e3 * sorted(lat)[int(0.9 * runs)],
+            "runs": runs}
+
+
 def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
     """The C++ CPU restatement (oracle/cpu, BlsMultiThreadWorkerPool policy: packages of
     >= 128 sets over `threads` workers, >= 16-job batch chunks, per-job retry) timed on
@@ -152,6 +199,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=8192, help="jobs per pass timed on the host CPU (cpu_baseline)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum host-CPU time of the cpu_baseline sample")
+    ap.add_argument("--no-block-import", action="store_true", help="skip the config-3 latency measurement")
     args = ap.parse_args()
     rank, world, local = dist_env()
     barrier = Barrier(world)
@@ -206,6 +254,9 @@ def main():
         raise SystemExit("verdict mismatch")
     elapsed = barrier.max(elapsed)
     kms, launches = ctx.profile(0)
+    block = None
+    if rank == 0 and not args.no_block_import and args.nkeys >= 16896:  # outside the timed region
+        block = block_import_latency(ctx, native, args.nkeys)
 
     if rank == 0:
         total_sets = args.nsets * args.steps * world
@@ -271,6 +322,8 @@ def main():
                          "pipeline_frac": pipeline_frac},
             "setup_s": setup_s,
         }
+        if block is not None:
+            line["block_import"] = block
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(jobs, key_of, expect, min(args.nsets, args.cpu_sample),
                                                 args.cpu_seconds)
