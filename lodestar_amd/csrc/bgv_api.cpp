@@ -665,6 +665,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   HIPCHK(x.h_verdict.reserve(std::max<size_t>(ngroups, 1)));
   bgv_dslot* slots = x.h_slots.p;
   bgv_dgroup* groups = x.h_groups.p;
+  uint32_t max_npk = 0;
   {
     size_t ns = 0, ng = 0, ni = 0, npb = 0;
     for (Call* call : calls) {
@@ -673,6 +674,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
         if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
         if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
         if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
+        max_npk = std::max(max_npk, s.n_pk);
         slots[ns++] = s;
       }
       for (bgv_dgroup g : call->L.groups) groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots};
@@ -697,6 +699,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, x.h_idx.p, 4 * nidx, hipMemcpyHostToDevice, x.main));
   if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, x.h_pkb.p, npkb, hipMemcpyHostToDevice, x.main));
   bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
+  b.max_npk = max_npk;
   bgv_streams S{x.main, prof ? x.kev : nullptr};
   bgv_streams SC{x.close, prof ? x.kev : nullptr};
   int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;

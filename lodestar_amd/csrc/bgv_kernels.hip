@@ -35,6 +35,11 @@
 #ifndef BGV_WPE_PREP
 #define BGV_WPE_PREP 2
 #endif
+// Sets with at least this many cached pubkeys are aggregated by k_pk_agg's wavefront
+// tree instead of serially on the set's k_prep lane.
+#ifndef BGV_PK_TREE_MIN
+#define BGV_PK_TREE_MIN 16
+#endif
 #define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
 #define BGV_KATTR_PREP __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_PREP, BGV_WPE_PREP)))
 
@@ -78,7 +83,7 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
                                      g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
-                                     const g1_aff* __restrict__ gtab) {
+                                     const g1_aff* __restrict__ gtab, const g1_jac* __restrict__ pk_agg) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
   if (d.flags & BGV_SLOT_PAD) {
@@ -87,7 +92,9 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
   }
   g1_jac acc = jac_infinity<fp_t>();
   const bool cached = (d.flags & BGV_SLOT_PK_CACHED) != 0;
-  for (uint32_t k = 0; k < d.n_pk; ++k) {
+  const bool tree = pk_agg != nullptr && cached && d.n_pk >= BGV_PK_TREE_MIN;  // summed by k_pk_agg
+  if (tree) acc = pk_agg[s];
+  for (uint32_t k = 0; k < (tree ? 0u : d.n_pk); ++k) {
     g1_aff a;
     if (cached) {
       a = cache[pk_idx[d.pk_off + k]];
@@ -121,6 +128,32 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
   pk_status[s] = st;
 }
 
+// Pubkey aggregation of many-key sets as a wavefront tree (one wave per slot): lane l
+// sums the set's cached keys l, l + 64, ... with mixed additions (coalesced gathers),
+// then six levels of complete Jacobian additions through LDS.  The sum is the same group
+// element as the serial one, so r * pk and its affine bytes are unchanged.  Waves of
+// slots with fewer than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane
+// reads the same slot), so no barrier is left waiting.
+__global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                               const uint32_t* __restrict__ pk_idx,
+                                               const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blockIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < BGV_PK_TREE_MIN) return;
+  __shared__ g1_jac t[64];
+  const uint32_t l = threadIdx.x;
+  g1_jac acc = jac_infinity<fp_t>();
+  for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
+  t[l] = acc;
+  __syncthreads();
+  for (uint32_t off = 32; off > 0; off >>= 1) {
+    if (l < off) t[l] = jac_add(t[l], t[l + off]);
+    __syncthreads();
+  }
+  if (l == 0) pk_agg[s] = t[0];
+}
+
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_aff* __restrict__ sig,
@@ -128,7 +161,7 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
                                  const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                  const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
                                  g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
-                                 const g1_aff* __restrict__ gtab) {
+                                 const g1_aff* __restrict__ gtab, const g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   // hash first: the longest task starts earliest
@@ -137,7 +170,7 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
   else if (blockIdx.y == 1)
     task_sig(s, slots, sig, sig_status);
   else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status, gtab);
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status, gtab, pk_agg);
 }
 
 // k_miller lives in bgv_miller_kernel.h; -DBGV_MILLER_SPLIT compiles it in its own
@@ -434,9 +467,14 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
   BGV_MARK(0);
+  // k_pk_agg only when some set is large enough; otherwise k_prep sums serially (null pk_agg)
+  const bool tree = b.max_npk >= BGV_PK_TREE_MIN;
+  if (tree)
+    hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
+                       reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
   hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.sig, b.sig_status, b.h,
                      b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.rg,
-                     b.pk_status, reinterpret_cast<const g1_aff*>(b.gtab));
+                     b.pk_status, reinterpret_cast<const g1_aff*>(b.gtab), tree ? b.pk_agg : nullptr);
   BGV_MARK(1);
   return hipGetLastError();
 }
@@ -469,7 +507,8 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
 #undef BGV_MARK
 
 size_t bgv_slot_bytes() {
-  return sizeof(g2_aff) + sizeof(g2_jac) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + 2 * sizeof(int32_t);
+  return sizeof(g2_aff) + sizeof(g2_jac) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + sizeof(g1_jac) +
+         2 * sizeof(int32_t);
 }
 size_t bgv_group_bytes() { return sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
@@ -486,6 +525,8 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   p += sizeof(g1_aff) * (size_t)cap_slots;
   b->f = reinterpret_cast<fp12_t*>(p);
   p += sizeof(fp12_t) * (size_t)cap_slots;
+  b->pk_agg = reinterpret_cast<g1_jac*>(p);
+  p += sizeof(g1_jac) * (size_t)cap_slots;
   b->sig_status = reinterpret_cast<int32_t*>(p);
   p += sizeof(int32_t) * (size_t)cap_slots;
   b->pk_status = reinterpret_cast<int32_t*>(p);

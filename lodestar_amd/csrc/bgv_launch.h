@@ -20,6 +20,7 @@ struct bgv_cache_entry;
 
 struct bgv_dev_batch {
   uint32_t nslots, ngroups;
+  uint32_t max_npk;  // largest n_pk of any slot (k_pk_agg runs only when a set reaches BGV_PK_TREE_MIN)
   const bgv_dslot* slots;
   const bgv_dgroup* groups;
   const uint32_t* pk_idx;
@@ -32,6 +33,7 @@ struct bgv_dev_batch {
   aff_t<fp_t>* rpk;   // r_i * aggregated pubkey
   aff_t<fp_t>* rg;    // r_i * (-G1)
   fp12_t* f;          // per-slot 2-pair Miller loop value
+  jac_t<fp_t>* pk_agg;  // wavefront-tree sum of a many-key set's cached pubkeys (k_pk_agg)
   int32_t* sig_status;
   int32_t* pk_status;
   int32_t* verdict;  // per group
