@@ -20,6 +20,8 @@ The JSON line carries:
   block_import config 3 of BASELINE.json, measured after the timed region: p50 latency of one
                non-batchable 131-set call (randao + 128 attestations x 128 keys + 512-key sync
                aggregate + proposer), one call at a time
+  aggregates_1024x128  config 2, also after the timed region: sets/s of 1024-set calls of
+               128-key aggregates (8 batchable jobs each), 32 calls in flight
 """
 import argparse
 import hashlib
@@ -157,6 +159,41 @@ def block_import_latency(ctx, native, nkeys, runs=100):
             "runs": runs}
 
 
+def aggregate_throughput(ctx, native, nkeys, calls=96, inflight=32):
+    """config 2: 1024 aggregate sets x 128 distinct cached keys (contiguous committees),
+    distinct signing roots, all valid, sent as the pool sends them (8 batchable jobs of
+    128 sets, index.ts:155-166); `calls` such calls, `inflight` at a time."""
+    from concurrent.futures import ThreadPoolExecutor
+    nsets, per = 1024, 128
+    assert nsets * per <= nkeys
+    sk_int = [int.from_bytes(interop_sk(i), "big") for i in range(nsets * per)]
+    msgs = [hashlib.sha256(b"lodestar-agg" + i.to_bytes(4, "little")).digest() for i in range(nsets)]
+    sks = [(sum(sk_int[per * a:per * a + per]) % R_ORDER).to_bytes(32, "big") for a in range(nsets)]
+    sigs = ctx.sign(b"".join(sks), b"".join(msgs))
+    sets = [native.SetSpec(msgs[a], sigs[96 * a:96 * a + 96], pk_indices=range(per * a, per * a + per))
+            for a in range(nsets)]
+    jobs = [(sets[j:j + 128], True) for j in range(0, nsets, 128)]
+    packed = native.PackedCall(jobs)
+
+    def call(_):
+        out = (native.ctypes.c_int32 * len(jobs))()
+        rc = ctx.lib.bgv_verify(ctx.handle, packed.jobs, len(jobs), packed.sets, packed.nsets, native.MODE_WORKER,
+                                out, None)
+        if rc != 0:
+            raise native.DeviceError(native.strerror(rc))
+        return list(out)
+
+    assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=inflight) as pool:
+        res = list(pool.map(call, range(calls)))
+    dt = time.perf_counter() - t0
+    assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
+    return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls, "
+                      "%d in flight" % (calls, inflight),
+            "value": nsets * calls / dt, "unit": "sets/s", "pubkeys_per_s": nsets * per * calls / dt}
+
+
 def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
     """The C++ CPU restatement (oracle/cpu, BlsMultiThreadWorkerPool policy: packages of
     >= 128 sets over `threads` workers, >= 16-job batch chunks, per-job retry) timed on
@@ -255,8 +292,11 @@ def main():
     elapsed = barrier.max(elapsed)
     kms, launches = ctx.profile(0)
     block = None
+    agg = None
     if rank == 0 and not args.no_block_import and args.nkeys >= 16896:  # outside the timed region
         block = block_import_latency(ctx, native, args.nkeys)
+    if rank == 0 and not args.no_block_import and args.nkeys >= 131072:
+        agg = aggregate_throughput(ctx, native, args.nkeys)
 
     if rank == 0:
         total_sets = args.nsets * args.steps * world
@@ -324,6 +364,8 @@ def main():
         }
         if block is not None:
             line["block_import"] = block
+        if agg is not None:
+            line["aggregates_1024x128"] = agg
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(jobs, key_of, expect, min(args.nsets, args.cpu_sample),
                                                 args.cpu_seconds)
