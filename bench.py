@@ -293,9 +293,10 @@ def main():
     kms, launches = ctx.profile(0)
     block = None
     agg = None
-    if rank == 0 and not args.no_block_import and args.nkeys >= 16896:  # outside the timed region
+    extras = world == 1 and not args.no_block_import  # N=1 only, outside the timed region
+    if extras and args.nkeys >= 16896:
         block = block_import_latency(ctx, native, args.nkeys)
-    if rank == 0 and not args.no_block_import and args.nkeys >= 131072:
+    if extras and args.nkeys >= 131072:
         agg = aggregate_throughput(ctx, native, args.nkeys)
 
     if rank == 0:
