@@ -315,9 +315,10 @@ def main():
         # whole-pipeline VALU figure: every verify kernel's counted work over the step time
         # closing: one final exponentiation per device group, and (at least) one Fp12
         # product per slot for the group products
-        per_group = opc["k_final[per group]"]
+        per_group = opc["k_final[per group]"] + opc["k_final[group sig pair]"]
         groups = statistics.mean(s.device_groups for s in stats)
-        pipeline_macs = ((sum(per_set.values()) + opc["k_final[per product step]"]) * slots + per_group * groups) \
+        per_slot_close = opc["k_final[per product step]"] + opc["k_final[per slot sig add]"]
+        pipeline_macs = ((sum(per_set.values()) + per_slot_close) * slots + per_group * groups) \
             * MACS_PER_FP_MUL * args.steps * world
         pipeline_frac = pipeline_macs / elapsed / (PEAK_MAC_PER_S * world)
         # HBM bytes per launch of the dominant kernel from the committed PMC passes

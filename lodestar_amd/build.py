@@ -27,29 +27,41 @@ def up_to_date(lib=LIB):
     return os.path.exists(lib) and all(os.path.getmtime(lib) >= os.path.getmtime(d) for d in deps())
 
 
+OBJ_DIR = os.path.join(HERE, "..", "build", "obj")
+
+
+def _headers():
+    out = [os.path.join(HERE, "..", "include", "blsgpu.h")]
+    return out + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+
+
 def build(force=False, verbose=True, lib=LIB, defines=()):
-    """defines: extra -D flags (tuning variants built to another `lib` path)."""
+    """defines: extra -D flags (tuning variants built to another `lib` path).  Objects are
+    cached per source under build/obj (the kernel unit takes minutes; the host unit seconds)
+    and rebuilt when the source or any header is newer."""
     if not force and up_to_date(lib):
         return lib
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    hdr_mtime = max(os.path.getmtime(h) for h in _headers())
     objs = []
-    srcs = list(SOURCES)
-    if "BGV_MILLER_SPLIT" in defines:  # k_miller in its own unit, Fp products inlined
-        srcs.insert(1, os.path.join(CSRC, "bgv_kernels_miller.hip"))
-    for src in srcs:
-        obj = os.path.join(CSRC, os.path.basename(lib) + "." + os.path.basename(src) + ".o")
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-c", src, "-o", obj] + ["-D" + d for d in defines]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+    tag = os.path.basename(lib) + ("." + "_".join(defines) if defines else "")
+    for src in SOURCES:
+        obj = os.path.join(OBJ_DIR, tag + "." + os.path.basename(src) + ".o")
+        fresh = (not force and os.path.exists(obj)
+                 and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime))
+        if not fresh:
+            cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+                   "-c", src, "-o", obj + ".tmp"] + ["-D" + d for d in defines]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.check_call(cmd)
+            os.replace(obj + ".tmp", obj)
         objs.append(obj)
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(lib + ".tmp", lib)
-    for o in objs:
-        os.remove(o)
     return lib
 
 

@@ -144,7 +144,6 @@ struct Device {
   int id = 0;
   hipStream_t stream = nullptr;      // utility work (cache upload, hooks, keygen)
   bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
-  void* gtab = nullptr;               // fixed-base multiples of -G1 (built at init)
   size_t cache_cap = 0;
   std::vector<Exec*> execs;
   // held while one super-batch runs its per-set kernels (pointer: Device stays movable)
@@ -270,6 +269,9 @@ struct bgv_ctx {
   std::mutex util_mu;          // utility streams
   std::mutex prof_mu;
   bool profile = false;
+  // BGV_FAULT_INJECT=1 at bgv_init: every super-batch fails as a HIP error would (tests of
+  // the device-error path: every job in flight rejects with BGV_E_DEVICE, none resolves false)
+  bool fault_inject = false;
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
   // dispatch
@@ -411,7 +413,6 @@ static bgv_dev_batch make_batch(Device& d, Exec& x, uint32_t nslots, uint32_t ng
   b.groups = x.d_groups;
   b.pk_idx = x.d_idx;
   b.cache_opaque = d.cache;
-  b.gtab = d.gtab;
   b.pk_bytes = x.d_pkb;
   bgv_carve(&b, x.slot_mem, x.slot_cap, x.group_mem, x.group_cap);
   return b;
@@ -694,6 +695,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     prof = c->profile;
   }
   t_merge = ms_since(tb);
+  if (c->fault_inject) HIPCHK(hipErrorLaunchFailure);
   HIPCHK(hipMemcpyAsync(x.d_slots, slots, sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
   HIPCHK(hipMemcpyAsync(x.d_groups, groups, sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
   if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, x.h_idx.p, 4 * nidx, hipMemcpyHostToDevice, x.main));
@@ -722,7 +724,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   }
   const auto tg = std::chrono::steady_clock::now();
   HIPCHK(hipStreamWaitEvent(x.close, x.ev_sets, 0));
-  HIPCHK(bgv_launch_groups(b, SC));
+  HIPCHK(bgv_launch_groups(b, SC, false));
   HIPCHK(hipEventRecord(x.ev1, x.close));
   HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
   HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
@@ -763,7 +765,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
     b = make_batch(d, x, nslots, nrg);
     HIPCHK(hipEventRecord(x.ev0, x.close));
-    HIPCHK(bgv_launch_groups(b, SC));
+    HIPCHK(bgv_launch_groups(b, SC, true));
     HIPCHK(hipEventRecord(x.ev1, x.close));
     HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
     HIPCHK(hipStreamSynchronize(x.close));
@@ -846,8 +848,6 @@ static void ctx_free_devices(bgv_ctx* c) {
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
-    if (d.gtab) (void)hipFree(d.gtab);
-    d.gtab = nullptr;
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.stream = nullptr;
   }
@@ -859,15 +859,17 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   int avail = bgv_device_count();
   if (avail <= 0) return -BGV_E_DEVICE;
   bgv_ctx* c = new bgv_ctx();
+  {
+    const char* fi = getenv("BGV_FAULT_INJECT");
+    c->fault_inject = fi && atoi(fi) > 0;
+  }
   const int n = (devices && ndev > 0) ? ndev : 1;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
     Device& d = c->devs[i];
     d.id = (devices && ndev > 0) ? devices[i] : 0;
     bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
-              hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess &&
-              hipMalloc(&d.gtab, bgv_gtab_bytes()) == hipSuccess && bgv_launch_gtab(d.gtab, d.stream) == hipSuccess &&
-              hipStreamSynchronize(d.stream) == hipSuccess;
+              hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
       Exec* x = new Exec();
       d.execs.push_back(x);
@@ -940,8 +942,8 @@ static int cache_reserve(bgv_ctx* c, size_t need) {
 
 int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, int fmt) {
   if (!c || (n && !keys) || (fmt != BGV_PK_COMPRESSED && fmt != BGV_PK_UNCOMPRESSED)) return -BGV_E_ARG;
-  if (c->closed) return -BGV_E_CLOSED;
   std::unique_lock<std::shared_mutex> lk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
   if ((size_t)first > c->n_pubkeys) return -BGV_E_ARG;  // append or overwrite, no holes
   if (n == 0) return BGV_OK;
   const size_t need = (size_t)first + n;
@@ -1005,29 +1007,40 @@ int bgv_verify_async(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_se
 
 int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out96[96]) {
   if (!c || !out96 || (n && !idx)) return -BGV_E_ARG;
-  if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return -BGV_E_EMPTY_AGGREGATE;
   std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
   for (size_t i = 0; i < n; ++i)
     if (idx[i] >= c->n_pubkeys) return -BGV_E_BAD_INDEX;
   std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];
   HIPCHK(hipSetDevice(d.id));
+  // one cached-key slot through the verify path's aggregation (k_pk_agg / pk_sum)
+  bgv_dslot s;
+  memset(&s, 0, sizeof(s));
+  s.flags = BGV_SLOT_PK_CACHED;
+  s.n_pk = (uint32_t)n;
   uint32_t* di = nullptr;
   uint8_t* dout = nullptr;
+  bgv_dslot* ds = nullptr;
+  void* dagg = nullptr;
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&di), 4 * n));
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&dout), 96));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&ds), sizeof(bgv_dslot)));
+  HIPCHK(hipMalloc(&dagg, bgv_g1_point_bytes()));
   HIPCHK(hipMemcpyAsync(di, idx, 4 * n, hipMemcpyHostToDevice, d.stream));
-  HIPCHK(bgv_launch_aggregate(di, (uint32_t)n, d.cache, dout, d.stream));
+  HIPCHK(hipMemcpyAsync(ds, &s, sizeof(s), hipMemcpyHostToDevice, d.stream));
+  HIPCHK(bgv_launch_aggregate(ds, di, (uint32_t)n, d.cache, dagg, dout, d.stream));
   HIPCHK(hipMemcpyAsync(out96, dout, 96, hipMemcpyDeviceToHost, d.stream));
   HIPCHK(hipStreamSynchronize(d.stream));
-  (void)hipFree(di);
-  (void)hipFree(dout);
+  void* bufs[] = {di, dout, ds, dagg};
+  for (void* p : bufs) (void)hipFree(p);
   return BGV_OK;
 }
 
 int bgv_hash_to_g2(bgv_ctx* c, const uint8_t* msgs, const uint32_t* lens, size_t n, uint8_t* out192) {
   if (!c || (n && (!lens || !out192))) return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);  // bgv_close frees the devices under the exclusive lock
   if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return BGV_OK;
   std::vector<uint32_t> offs(n);
@@ -1062,6 +1075,7 @@ int bgv_hash_to_g2(bgv_ctx* c, const uint8_t* msgs, const uint32_t* lens, size_t
 
 int bgv_pubkeys_validate(bgv_ctx* c, const uint8_t* keys48, size_t n, int32_t* out_status, uint8_t* out96) {
   if (!c || (n && (!keys48 || !out_status))) return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);  // bgv_close frees the devices under the exclusive lock
   if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return BGV_OK;
   std::lock_guard<std::mutex> lk(c->util_mu);
@@ -1087,6 +1101,7 @@ int bgv_pubkeys_validate(bgv_ctx* c, const uint8_t* keys48, size_t n, int32_t* o
 int bgv_aggregate_signatures(bgv_ctx* c, const uint8_t* sigs96, const uint32_t* lens, const uint32_t* counts,
                              size_t naggs, uint8_t* out96, int32_t* out_status) {
   if (!c || (naggs && (!counts || !out96 || !out_status))) return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);  // bgv_close frees the devices under the exclusive lock
   if (c->closed) return -BGV_E_CLOSED;
   if (naggs == 0) return BGV_OK;
   std::vector<uint32_t> first(naggs);
@@ -1171,8 +1186,8 @@ int bgv_deposits_verify(bgv_ctx* c, const uint8_t* keys48, const uint8_t* msgs32
 
 int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48) {
   if (!c || (n && !sks)) return -BGV_E_ARG;
-  if (c->closed) return -BGV_E_CLOSED;
   std::unique_lock<std::shared_mutex> clk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
   if (cache_first > (int64_t)c->n_pubkeys) return -BGV_E_ARG;
   if (n == 0) return BGV_OK;
   if (cache_first >= 0) {
@@ -1203,6 +1218,7 @@ int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, ui
 
 int bgv_sign(bgv_ctx* c, const uint8_t* sks, const uint8_t* msgs, size_t n, uint8_t* out96) {
   if (!c || (n && (!sks || !msgs || !out96))) return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);  // bgv_close frees the devices under the exclusive lock
   if (c->closed) return -BGV_E_CLOSED;
   if (n == 0) return BGV_OK;
   std::lock_guard<std::mutex> lk(c->util_mu);

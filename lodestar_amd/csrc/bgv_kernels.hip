@@ -3,22 +3,24 @@
 // One signature set per lane.  A verify call runs these kernels in order (see
 // bgv_api.cpp):
 //
+//   k_pk_agg   (only when a call holds a set with >= BGV_PK_TREE_MIN cached keys) one
+//              wavefront per such set sums its keys with a ds_swizzle/ds_bpermute tree
 //   k_prep     three independent tasks side by side (blockIdx.y):
-//              sig  decompress + subgroup-check the 96-byte signature -> affine sig_i
-//              hash hash_to_G2(signing root) -> affine H(m_i)
-//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i and
-//                   r_i * (-G1), both made affine with one shared inversion
-//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)) * MillerLoop(-r_i G1, sig_i), one
-//              shared Fp12 accumulator (2-pair loop)
-//   k_final    per device group (a team of 16 lanes): prod f_i over the group's
-//              slots, then the final-exponentiation check -> == 1
+//              sig  decompress + subgroup-check the 96-byte signature, then r_i * sig_i
+//                   (Jacobian G2, summed per group by the closing)
+//              hash hash_to_G2(signing root) -> H(m_i), Jacobian
+//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i, affine
+//   k_gsum     per device group (a team of 16 lanes): S_g = sum of the group's r_i sig_i
+//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)), one pair per lane, and on extra lanes
+//              one per group g_g = MillerLoop(-G1, S_g) (retry rounds: k_gpair)
+//   k_final    per device group (a team of 16 lanes): prod f_i * g_g and the
+//              final-exponentiation check -> == 1
 //
 // This is the randomized batch equation of blst's verifyMultipleAggregateSignatures
 // (called from packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25):
 //   prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i) == 1,
-// with e(-G1, sum r_i sig_i) = prod_i e(-r_i G1, sig_i) moved into the per-set
-// kernel, so a group closes with a product and one final exponentiation only.
-// A one-set group is the core verify of maybeBatch.ts:34-38 raised to the
+// with blst's structure: one pair per set, r_i sig_i in G2, one signature pair per
+// group.  A one-set group is the core verify of maybeBatch.ts:34-38 raised to the
 // power r (nonzero, < group order), which has the same verdict.
 #include "bgv_layout.h"
 #define BGV_KERNEL_SIDE 1
@@ -43,9 +45,32 @@
 #define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
 #define BGV_KATTR_PREP __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_PREP, BGV_WPE_PREP)))
 
+// Wavefront exchange of one 32-bit word with lane (l ^ m): ds_swizzle in bit-mask mode
+// within each 32-lane half (m < 32), ds_bpermute across the halves (m = 32).  No LDS
+// storage is allocated: both go through the LDS crossbar only.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (M == 32)
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32u) << 2), (int)v);
+  else
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (M << 10));  // and 0x1f, xor M
+}
+
+template <int M, class P>
+__device__ __forceinline__ P point_xor(const P& p) {
+  constexpr int W = (int)(sizeof(P) / 4);
+  P r;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+  BGV_UNROLL for (int i = 0; i < W; ++i) o[i] = lane_xor<M>(a[i]);
+  return r;
+}
+
+
 extern "C" {
 
-__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* __restrict__ sig,
+// r_i * sig_i of a set whose signature decodes and lies in G2 (else only a status).
+__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
                                       int32_t* __restrict__ sig_status) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
@@ -60,12 +85,15 @@ __device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ 
     bool inf;
     st = g2_decompress(&a, &inf, b);
     if (st == BGV_OK) {
-      if (inf)
+      if (inf) {
         st = BGV_ST_INFINITY;  // skipped in the accumulator, as blst does
-      else if (!g2_in_subgroup(jac_from_aff(a)))
-        st = BGV_POINT_NOT_IN_GROUP;
-      else
-        sig[s] = a;
+      } else {
+        const g2_jac j = jac_from_aff(a);
+        if (!g2_in_subgroup(j))
+          st = BGV_POINT_NOT_IN_GROUP;
+        else
+          rsig[s] = jac_mul_u64(j, d.scalar);  // never infinity: 0 < r < group order
+      }
     }
   }
   sig_status[s] = st;
@@ -79,22 +107,18 @@ __device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__
   h[s] = hash_to_g2(msg, 32);  // stays Jacobian: k_miller adds it with miller_add_jq
 }
 
-__device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
-                                     const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                     const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                     g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
-                                     const g1_aff* __restrict__ gtab, const g1_jac* __restrict__ pk_agg) {
-  const bgv_dslot& d = slots[s];
-  int32_t st = BGV_ST_OK;
-  if (d.flags & BGV_SLOT_PAD) {
-    pk_status[s] = BGV_ST_INFINITY;
-    return;
-  }
+// Sum of one set's pubkeys (PublicKey.aggregate, chain/bls/utils.ts:5-16): the k_pk_agg
+// tree sum when the set went through it, else serial mixed additions of cached keys or of
+// 96-byte records (decoded like blst's PublicKey.fromBytes, bls_curve.h g1_deserialize).
+// *st receives the first record's decode error, if any.
+__device__ __noinline__ static g1_jac pk_sum(const bgv_dslot& d, const uint32_t* __restrict__ pk_idx,
+                                      const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
+                                      const g1_jac* __restrict__ pk_agg, uint32_t s, int32_t* st) {
   g1_jac acc = jac_infinity<fp_t>();
   const bool cached = (d.flags & BGV_SLOT_PK_CACHED) != 0;
   const bool tree = pk_agg != nullptr && cached && d.n_pk >= BGV_PK_TREE_MIN;  // summed by k_pk_agg
-  if (tree) acc = pk_agg[s];
-  for (uint32_t k = 0; k < (tree ? 0u : d.n_pk); ++k) {
+  if (tree) return pk_agg[s];
+  for (uint32_t k = 0; k < d.n_pk; ++k) {
     g1_aff a;
     if (cached) {
       a = cache[pk_idx[d.pk_off + k]];
@@ -104,36 +128,44 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
       for (int i = 0; i < 96; ++i) b[i] = src[i];
       bool inf;
       const int rc = g1_deserialize(&a, &inf, b);
-      if (rc == BGV_OK && !inf && !g1_aff_on_curve(a)) st = BGV_POINT_NOT_ON_CURVE;
-      else if (rc != BGV_OK) st = rc;
-      if (st != BGV_OK) break;
+      if (rc != BGV_OK) {
+        *st = rc;
+        break;
+      }
       if (inf) continue;
     }
     acc = jac_add_aff(acc, a);
   }
+  return acc;
+}
+
+__device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
+                                     const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                     const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                     int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  if (d.flags & BGV_SLOT_PAD) {
+    pk_status[s] = BGV_ST_INFINITY;
+    return;
+  }
+  const g1_jac acc = pk_sum(d, pk_idx, cache, pk_bytes, pk_agg, s, &st);
   if (st == BGV_OK) {
-    const g1_jac a = jac_mul_u64(acc, d.scalar);
-    if (jac_is_inf(a)) {
-      st = BGV_ST_INFINITY;
-    } else {
-      // r_i * (-G1) for the signature's pair from the fixed-base table; never infinity
-      // (0 < r_i < group order)
-      const g1_jac g = g1_neg_gen_mul(gtab, d.scalar);
-      g1_aff pa, ga;
-      jac2_to_aff(&pa, &ga, a, g);
+    g1_aff pa;
+    if (!jac_to_aff(&pa, jac_mul_u64(acc, d.scalar)))
+      st = BGV_ST_INFINITY;  // infinity aggregate: BLST_PK_IS_INFINITY / false (job_precheck)
+    else
       rpk[s] = pa;
-      rg[s] = ga;
-    }
   }
   pk_status[s] = st;
 }
 
 // Pubkey aggregation of many-key sets as a wavefront tree (one wave per slot): lane l
 // sums the set's cached keys l, l + 64, ... with mixed additions (coalesced gathers),
-// then six levels of complete Jacobian additions through LDS.  The sum is the same group
-// element as the serial one, so r * pk and its affine bytes are unchanged.  Waves of
-// slots with fewer than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane
-// reads the same slot), so no barrier is left waiting.
+// then six butterfly levels of complete Jacobian additions with the partner lane's
+// partial sum (lane ^ 32, 16, ..., 1) exchanged in registers.  Every lane ends with the
+// total; the sum is the same group element as the serial one.  Waves of slots with fewer
+// than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane reads the same slot).
 __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                                const uint32_t* __restrict__ pk_idx,
                                                const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
@@ -141,49 +173,70 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   if (s >= nslots) return;
   const bgv_dslot& d = slots[s];
   if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < BGV_PK_TREE_MIN) return;
-  __shared__ g1_jac t[64];
   const uint32_t l = threadIdx.x;
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
-  t[l] = acc;
-  __syncthreads();
-  for (uint32_t off = 32; off > 0; off >>= 1) {
-    if (l < off) t[l] = jac_add(t[l], t[l + off]);
-    __syncthreads();
-  }
-  if (l == 0) pk_agg[s] = t[0];
+  acc = jac_add(acc, point_xor<32>(acc));
+  acc = jac_add(acc, point_xor<16>(acc));
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (l == 0) pk_agg[s] = acc;
 }
 
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
-__global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_aff* __restrict__ sig,
-                                 int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
-                                 const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                 const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
-                                 g1_aff* __restrict__ rg, int32_t* __restrict__ pk_status,
-                                 const g1_aff* __restrict__ gtab, const g1_jac* __restrict__ pk_agg) {
+__global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
+                                      int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
+                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   // hash first: the longest task starts earliest
   if (blockIdx.y == 0)
     task_hash(s, slots, h);
   else if (blockIdx.y == 1)
-    task_sig(s, slots, sig, sig_status);
+    task_sig(s, slots, rsig, sig_status);
   else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, rg, pk_status, gtab, pk_agg);
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
 }
 
-// k_miller lives in bgv_miller_kernel.h; -DBGV_MILLER_SPLIT compiles it in its own
-// translation unit (bgv_kernels_miller.hip) with the Fp products inlined.
-#ifdef BGV_MILLER_SPLIT
+// A slot takes part in its group's equation iff it is a set whose signature decoded
+// (valid or infinity) and whose pubkeys aggregated to a finite point; its signature
+// joins the group's sum only when it is not the infinity signature (blst skips those).
+__device__ __forceinline__ bool slot_live(const bgv_dslot& d, int32_t ss, int32_t ps) {
+  return !(d.flags & BGV_SLOT_PAD) && (ss == BGV_ST_OK || ss == BGV_ST_INFINITY) && ps == BGV_ST_OK;
+}
+
+// Lanes [0, nslots): f_i = MillerLoop(r pk, H(m)), 1 for slots that do not take part.
+// Lanes [nslots, nslots + ngroups): the group's signature pair MillerLoop(-G1, S_g) (1 for
+// an infinite S_g), so the group pairs run beside the set pairs instead of after them.
+__device__ __forceinline__ fp12_t group_pair(const g2_jac& S) {
+  return jac_is_inf(S) ? fp12_one() : miller_loop1(g1_neg_generator(), S);
+}
+
 __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                    const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
-                                   const g1_aff* __restrict__ rg, const g2_aff* __restrict__ sig,
                                    const int32_t* __restrict__ sig_status, const int32_t* __restrict__ pk_status,
-                                   fp12_t* __restrict__ f);
-#else
-#include "bgv_miller_kernel.h"
-#endif
+                                   fp12_t* __restrict__ f, uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                   fp12_t* __restrict__ gpair) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < nslots) {
+    fp12_t r = fp12_one();
+    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1(rpk[s], h[s]);
+    f[s] = r;
+  } else if (s - nslots < ngroups) {
+    gpair[s - nslots] = group_pair(gsum[s - nslots]);
+  }
+}
+
+// retry rounds: the signature pairs of the round's parts alone
+__global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ngroups) gpair[g] = group_pair(gsum[g]);
+}
 
 // Group closing, team-parallel (bls_team.h): a team of 16 lanes per group, lane c < 12
 // owning one Fp coefficient of the running value; operands exchanged through LDS.
@@ -212,6 +265,14 @@ struct tm_dev_ops {
     __syncthreads();
     return r;
   }
+  __device__ fp_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) { return tm_line_lane(cc, l0, l1, l3); }
+  __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t r = tm_mul_line_lane(cc, A, l0, l1, l3);
+    __syncthreads();
+    return r;
+  }
   __device__ fp_t conj(const fp_t& x) { return fp_select(((cc >> 1) & 1) != 0, x, fp_neg(x)); }
   __device__ fp_t frob(const fp_t& x) {
     if (c < BGV_TEAM_COMPS) A[c] = x;
@@ -229,31 +290,59 @@ struct tm_dev_ops {
 };
 
 #define BGV_FINAL_TEAMS (64 / BGV_TEAM)
-// One team per device group: the product of the group's per-slot f_i (coefficient-
-// parallel team products, operands straight from the per-slot array), then the
-// final-exponentiation check.  The teams of a wave loop to the wave's longest group,
-// the shorter ones multiplying by 1, so every lane reaches every barrier.
+// S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an
+// infinity signature in the accumulator).  A team of 16 lanes per group: lane c sums
+// every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
+__global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                             const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
+                                             const int32_t* __restrict__ sig_status,
+                                             const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum) {
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  g2_jac acc = jac_infinity<fp2_t>();
+  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+    const uint32_t s = g.first_slot + k;
+    const int32_t ss = sig_status[s];
+    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+  }
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (gi < ngroups && c == 0) gsum[gi] = acc;
+}
+
+// One team per device group (first pass: the groups of the layout; retry rounds: parts of
+// failed groups), each a contiguous range of <= 64 slots: v = prod f_i * g_g with
+// coefficient-parallel team products (operands straight from the per-slot array), then
+// the final-exponentiation check v^((p^12-1)/r) == 1.  The teams of a wave loop to the
+// wave's longest group, the shorter ones multiplying by 1, so every lane reaches every
+// barrier.
 __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
-                                  const fp12_t* __restrict__ f, int32_t* __restrict__ verdict) {
+                                  const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
+                                  int32_t* __restrict__ verdict) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL_TEAMS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   // teams past the end duplicate the last group
-  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  const uint32_t gg = gi < ngroups ? gi : ngroups - 1;
+  const bgv_dgroup g = groups[gg];
   if (c == 0) lens[team] = g.n_slots;
   __syncthreads();
   uint32_t nmax = 0;
   BGV_UNROLL for (int t = 0; t < BGV_FINAL_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
   const int fi = tm_fp_index(cc);
   const fp_t one_c = cc == 0 ? fp_one() : fp_zero();  // component cc of 1
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
   const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
   constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
-  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
-  fp_t x = g.n_slots ? fs[fi] : one_c;
-  fp_t y = 1 < g.n_slots ? fs[kFp12 + fi] : one_c;
-  BGV_NO_UNROLL for (uint32_t k = 1; k < nmax; ++k) {
+  // the group's signature pair first, then its slots
+  fp_t x = reinterpret_cast<const fp_t*>(gpair + gg)[fi];
+  fp_t y = g.n_slots ? fs[fi] : one_c;
+  BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
     const fp_t yn = k + 1 < g.n_slots ? fs[kFp12 * (k + 1) + fi] : one_c;  // next operand in flight
     x = o.mul(x, y);
     y = yn;
@@ -262,11 +351,15 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
   if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
-__global__ void k_aggregate_cached(const uint32_t* __restrict__ idx, uint32_t n, const g1_aff* __restrict__ cache,
-                                   uint8_t* __restrict__ out96) {
+// PublicKey.aggregate(...).toBytes(uncompressed) over cached keys through the verify
+// path's own code: pk_sum of one slot (k_pk_agg's tree sum for >= BGV_PK_TREE_MIN keys,
+// task_pk's serial sum below), then affine and the 96-byte ZCash encoding.
+__global__ void k_pk_sum_out(const bgv_dslot* __restrict__ slot, const uint32_t* __restrict__ idx,
+                             const g1_aff* __restrict__ cache, const g1_jac* __restrict__ pk_agg,
+                             uint8_t* __restrict__ out96) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  g1_jac acc = jac_infinity<fp_t>();
-  for (uint32_t k = 0; k < n; ++k) acc = jac_add_aff(acc, cache[idx[k]]);
+  int32_t st = BGV_OK;
+  const g1_jac acc = pk_sum(slot[0], idx, cache, nullptr, pk_agg, 0, &st);
   g1_aff a;
   const bool fin = jac_to_aff(&a, acc);
   uint8_t b[96];
@@ -358,10 +451,6 @@ __global__ void BGV_KATTR k_sig_sum(const uint32_t* __restrict__ first, const ui
   }
 }
 
-__global__ void k_gtab_build(g1_aff* __restrict__ tab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < BGV_GTAB_ENTRIES) tab[i] = g1_gtab_entry(i);
-}
 
 __global__ void k_hash_msgs(const uint8_t* __restrict__ msgs, const uint32_t* __restrict__ offs,
                             const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ out192) {
@@ -400,7 +489,6 @@ __global__ void k_cache_put_uncompressed(const uint8_t* __restrict__ keys, uint3
   bool inf;
   int rc = g1_deserialize(&a, &inf, b);
   if (rc == BGV_OK && inf) rc = BGV_PK_IS_INFINITY;
-  if (rc == BGV_OK && !g1_aff_on_curve(a)) rc = BGV_POINT_NOT_ON_CURVE;
   if (rc == BGV_OK) cache[i] = a;
   status[i] = rc;
 }
@@ -472,9 +560,9 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   if (tree)
     hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
                        reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
-  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.sig, b.sig_status, b.h,
-                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.rg,
-                     b.pk_status, reinterpret_cast<const g1_aff*>(b.gtab), tree ? b.pk_agg : nullptr);
+  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
+                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
+                     tree ? b.pk_agg : nullptr);
   BGV_MARK(1);
   return hipGetLastError();
 }
@@ -482,9 +570,12 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
+  // the groups' signature sums, then set pairs and group pairs in one launch
+  hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                     b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
   BGV_MARK(2);
-  hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.rg, b.sig,
-                     b.sig_status, b.pk_status, b.f);
+  hipLaunchKernelGGL(k_miller, dim3(nblk(n + b.ngroups, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h,
+                     b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
   BGV_MARK(3);
   return hipGetLastError();
 }
@@ -494,34 +585,37 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
   return e != hipSuccess ? e : bgv_launch_miller(b, s);
 }
 
-// Per-group kernels over b.groups (contiguous slot ranges of <= 64 slots): used for
-// the first pass and, over the same per-slot results, for the per-job retry pass.
-hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s) {
+// Group closing over b.groups (contiguous slot ranges of <= 64 slots) after
+// bgv_launch_miller (first pass, group pairs already made) or, for a retry round over the
+// same per-slot results, with pairs = true: the parts' signature sums and pairs first.
+hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs) {
   if (b.ngroups == 0) return hipSuccess;
   BGV_MARK(4);
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups, b.f,
-                     b.verdict);
+  if (pairs) {
+    hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                       b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
+    hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.ngroups, b.gsum, b.gpair);
+  }
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                     b.f, b.gpair, b.verdict);
   BGV_MARK(5);
   return hipGetLastError();
 }
 #undef BGV_MARK
 
 size_t bgv_slot_bytes() {
-  return sizeof(g2_aff) + sizeof(g2_jac) + 2 * sizeof(g1_aff) + sizeof(fp12_t) + sizeof(g1_jac) +
-         2 * sizeof(int32_t);
+  return 2 * sizeof(g2_jac) + sizeof(g1_aff) + sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t);
 }
-size_t bgv_group_bytes() { return sizeof(int32_t); }
+size_t bgv_group_bytes() { return sizeof(g2_jac) + sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
 
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
   uint8_t* p = static_cast<uint8_t*>(slot_mem);
-  b->sig = reinterpret_cast<g2_aff*>(p);
-  p += sizeof(g2_aff) * (size_t)cap_slots;
+  b->rsig = reinterpret_cast<g2_jac*>(p);
+  p += sizeof(g2_jac) * (size_t)cap_slots;
   b->h = reinterpret_cast<g2_jac*>(p);
   p += sizeof(g2_jac) * (size_t)cap_slots;
   b->rpk = reinterpret_cast<g1_aff*>(p);
-  p += sizeof(g1_aff) * (size_t)cap_slots;
-  b->rg = reinterpret_cast<g1_aff*>(p);
   p += sizeof(g1_aff) * (size_t)cap_slots;
   b->f = reinterpret_cast<fp12_t*>(p);
   p += sizeof(fp12_t) * (size_t)cap_slots;
@@ -530,8 +624,12 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   b->sig_status = reinterpret_cast<int32_t*>(p);
   p += sizeof(int32_t) * (size_t)cap_slots;
   b->pk_status = reinterpret_cast<int32_t*>(p);
-  (void)cap_groups;
-  b->verdict = static_cast<int32_t*>(group_mem);
+  uint8_t* q = static_cast<uint8_t*>(group_mem);
+  b->gsum = reinterpret_cast<g2_jac*>(q);
+  q += sizeof(g2_jac) * (size_t)cap_groups;
+  b->gpair = reinterpret_cast<fp12_t*>(q);
+  q += sizeof(fp12_t) * (size_t)cap_groups;
+  b->verdict = reinterpret_cast<int32_t*>(q);
 }
 
 hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_cache_entry* cache, int32_t* status,
@@ -545,10 +643,14 @@ hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_ca
   return hipGetLastError();
 }
 
-hipError_t bgv_launch_aggregate(const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache, uint8_t* out96,
-                                hipStream_t st) {
-  hipLaunchKernelGGL(k_aggregate_cached, dim3(1), dim3(64), 0, st, idx, n, reinterpret_cast<const g1_aff*>(cache),
-                     out96);
+// slot: one device bgv_dslot {PK_CACHED, n_pk = n, pk_off = 0}; agg: one g1_jac of scratch
+hipError_t bgv_launch_aggregate(const bgv_dslot* slot, const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache,
+                                void* agg, uint8_t* out96, hipStream_t st) {
+  const g1_aff* c = reinterpret_cast<const g1_aff*>(cache);
+  g1_jac* a = reinterpret_cast<g1_jac*>(agg);
+  const bool tree = n >= BGV_PK_TREE_MIN;
+  if (tree) hipLaunchKernelGGL(k_pk_agg, dim3(1), dim3(64), 0, st, slot, 1u, idx, c, a);
+  hipLaunchKernelGGL(k_pk_sum_out, dim3(1), dim3(64), 0, st, slot, idx, c, tree ? a : nullptr, out96);
   return hipGetLastError();
 }
 
@@ -580,12 +682,7 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
   return hipGetLastError();
 }
 size_t bgv_g2_point_bytes() { return sizeof(g2_jac); }
-size_t bgv_gtab_bytes() { return sizeof(g1_aff) * BGV_GTAB_ENTRIES; }
-hipError_t bgv_launch_gtab(void* tab, hipStream_t st) {
-  hipLaunchKernelGGL(k_gtab_build, dim3(BGV_GTAB_ENTRIES / 64), dim3(64), 0, st, reinterpret_cast<g1_aff*>(tab));
-  return hipGetLastError();
-}
-
+size_t bgv_g1_point_bytes() { return sizeof(g1_jac); }
 hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_keygen, dim3(nblk(n, 64)), dim3(64), 0, st, sks, n, reinterpret_cast<g1_aff*>(cache), out48);

@@ -26,17 +26,17 @@ struct bgv_dev_batch {
   const uint32_t* pk_idx;
   const bgv_cache_entry* cache_opaque;
   const uint8_t* pk_bytes;
-  const void* gtab;  // fixed-base table of multiples of -G1 (bgv_launch_gtab)
   // carved per-slot / per-group scratch
-  aff_t<fp2_t>* sig;  // decompressed signatures
-  jac_t<fp2_t>* h;    // H(m_i), Jacobian
-  aff_t<fp_t>* rpk;   // r_i * aggregated pubkey
-  aff_t<fp_t>* rg;    // r_i * (-G1)
-  fp12_t* f;          // per-slot 2-pair Miller loop value
+  jac_t<fp2_t>* rsig;  // r_i * sig_i (Jacobian), summed per group by k_final
+  jac_t<fp2_t>* h;     // H(m_i), Jacobian
+  aff_t<fp_t>* rpk;    // r_i * aggregated pubkey, affine
+  fp12_t* f;           // per-slot Miller loop value e(r_i pk_i, H(m_i))
   jac_t<fp_t>* pk_agg;  // wavefront-tree sum of a many-key set's cached pubkeys (k_pk_agg)
   int32_t* sig_status;
   int32_t* pk_status;
-  int32_t* verdict;  // per group
+  jac_t<fp2_t>* gsum;  // per group: sum of its r_i sig_i
+  fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
+  int32_t* verdict;    // per group
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
 #endif
@@ -53,15 +53,16 @@ struct bgv_streams {
 hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // prep + miller
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
-hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s);
+hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
 size_t bgv_slot_bytes();
 size_t bgv_group_bytes();
 size_t bgv_cache_entry_bytes();
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups);
 hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_cache_entry* cache, int32_t* status,
                                 hipStream_t st);
-hipError_t bgv_launch_aggregate(const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache, uint8_t* out96,
-                                hipStream_t st);
+hipError_t bgv_launch_aggregate(const bgv_dslot* slot, const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache,
+                                void* agg, uint8_t* out96, hipStream_t st);
+size_t bgv_g1_point_bytes();
 hipError_t bgv_launch_hash(const uint8_t* msgs, const uint32_t* offs, const uint32_t* lens, uint32_t n,
                            uint8_t* out192, hipStream_t st);
 hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st);
@@ -72,5 +73,3 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
                                     const uint32_t* count, uint32_t naggs, void* pts, int32_t* status,
                                     uint8_t* out96, hipStream_t st);
 size_t bgv_g2_point_bytes();
-size_t bgv_gtab_bytes();
-hipError_t bgv_launch_gtab(void* tab, hipStream_t st);

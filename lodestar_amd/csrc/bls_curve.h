@@ -276,32 +276,6 @@ BGV_HD g1_aff g1_neg_generator() {
   return g;
 }
 
-// Fixed-base table for r * (-G1) with 64-bit r: entry [j][k] = k * 2^(8j) * (-G1),
-// j < 8, 1 <= k < 256 (entry k = 0 unused).  2,040 affine points, 228 KB, built once
-// per device; a multiplication is then 8 mixed additions instead of ~96 group ops.
-#define BGV_GTAB_WINDOWS 8
-#define BGV_GTAB_ENTRIES (BGV_GTAB_WINDOWS * 256)
-BGV_HD g1_aff g1_gtab_entry(int idx) {
-  const int j = idx >> 8, k = idx & 255;
-  const uint32_t s[8] = {(uint32_t)((uint64_t)(k ? k : 1) << (8 * j)), (uint32_t)(((uint64_t)(k ? k : 1) << (8 * j)) >> 32),
-                         0, 0, 0, 0, 0, 0};
-  g1_aff a;
-  jac_to_aff(&a, jac_mul_u256(jac_from_aff(g1_neg_generator()), s));
-  return a;
-}
-
-// r * (-G1) from the table; r != 0 (no partial sum ever equals a table point or its
-// negation: every partial sum is a multiple below 2^64 of the group order's generator).
-BGV_NOINLINE g1_jac g1_neg_gen_mul(const g1_aff* __restrict__ tab, uint64_t r) {
-  g1_jac acc = jac_infinity<fp_t>();
-  BGV_NO_UNROLL for (int j = 0; j < BGV_GTAB_WINDOWS; ++j) {
-    const uint32_t d = (uint32_t)(r >> (8 * j)) & 255u;
-    const g1_jac sum = jac_add_aff(acc, tab[(j << 8) | (d ? d : 1)]);
-    acc = jac_select(d != 0, acc, sum);
-  }
-  return acc;
-}
-
 BGV_HD bool g1_aff_on_curve(const g1_aff& a) {
   const fp_t b = {BGV_B1};
   return fp_eq(fp_sqr(a.y), fp_add(fp_mul(fp_sqr(a.x), a.x), b));
@@ -427,12 +401,19 @@ BGV_HD void g2_serialize(uint8_t* b, const g2_aff& a, bool inf) {
   fp_to_be48(b + 144, fp_from_mont(a.y.c0));
 }
 
-// 96-byte uncompressed G1 (trusted pubkey bytes, worker.ts:110-116): no
-// subgroup or curve check; flags only.
+BGV_HD int g1_decompress(g1_aff* out, bool* inf, const uint8_t* b);
+
+// 96-byte G1 record (trusted pubkey bytes, worker.ts:110-116), decoded like blst's
+// POINTonE1_Deserialize_Z (PublicKey.fromBytes of 96 bytes): no subgroup check.
+//   top bits 000 -> big-endian x || y: x, y < p else BAD_ENCODING; on the curve else
+//                   POINT_NOT_ON_CURVE; x == 0 (the points (0, +-2)) -> POINT_NOT_IN_GROUP
+//   0x80 set     -> the first 48 bytes as a compressed point
+//   0x40 only    -> infinity iff every other bit is zero
+//   anything else (0x20 without 0x80 / 0x40) -> BAD_ENCODING
 BGV_HD int g1_deserialize(g1_aff* out, bool* inf, const uint8_t* b) {
   const uint8_t flags = b[0];
   *inf = false;
-  if (flags & 0x80) return BGV_BAD_ENCODING;
+  if (flags & 0x80) return g1_decompress(out, inf, b);
   if (flags & 0x40) {
     uint8_t acc = flags & 0x3f;
     for (int i = 1; i < 96; ++i) acc |= b[i];
@@ -440,14 +421,16 @@ BGV_HD int g1_deserialize(g1_aff* out, bool* inf, const uint8_t* b) {
     *inf = true;
     return BGV_OK;
   }
-  uint8_t tmp[48];
-  for (int i = 0; i < 48; ++i) tmp[i] = b[i];
-  tmp[0] &= 0x1f;
-  fp_t x = fp_from_be48(tmp);
+  if (flags & 0x20) return BGV_BAD_ENCODING;
+  fp_t x = fp_from_be48(b);
   fp_t y = fp_from_be48(b + 48);
   if (!fp_raw_lt_p(x) || !fp_raw_lt_p(y)) return BGV_BAD_ENCODING;
   out->x = fp_to_mont(x);
   out->y = fp_to_mont(y);
+  if (!g1_aff_on_curve(*out)) return BGV_POINT_NOT_ON_CURVE;
+  uint32_t nz = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) nz |= x.v[i];
+  if (nz == 0) return BGV_POINT_NOT_IN_GROUP;
   return BGV_OK;
 }
 
@@ -475,7 +458,10 @@ BGV_HD int g1_decompress(g1_aff* out, bool* inf, const uint8_t* b) {
   if (fp_lex_largest(y) != ((flags & 0x20) != 0)) y = fp_neg(y);
   out->x = x;
   out->y = y;
-  return BGV_OK;
+  // (0, +-2) is on the curve but of order 3: blst's POINTonE1_Uncompress_Z rejects it
+  uint32_t nz = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) nz |= xr.v[i];
+  return nz ? BGV_OK : BGV_POINT_NOT_IN_GROUP;
 }
 
 BGV_HD void g1_serialize(uint8_t* b, const g1_aff& a, bool inf) {

@@ -29,9 +29,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BGV_HD __host__ __device__ __forceinline__
-#ifndef BGV_NOINLINE  // bgv_kernels_miller.hip makes its copies static (one TU per kernel set)
 #define BGV_NOINLINE __host__ __device__ __noinline__
-#endif
 #else
 #define BGV_HD inline __attribute__((always_inline))
 #define BGV_NOINLINE __attribute__((noinline))
@@ -45,7 +43,7 @@
 #endif
 
 // The tower functions of the Miller-loop step (fp6_mul, fp6_mul_01, fp12_sqr, the
-// line products, miller_dbl/add) are inlined into miller_loop2, so f, T and the
+// line products, miller_dbl/add) are inlined into miller_loop1, so f, T and the
 // lines stay in VGPRs and only fp_mul/fp_sqr are calls: out of line, every
 // by-reference argument and struct return went through scratch, and at one wave
 // per SIMD nothing hid that latency (k_miller 51.4 -> 41.3 ms per 131,072 sets,
@@ -629,31 +627,6 @@ BGV_MILLER_ATTR fp12_t fp12_mul_line(const fp12_t& f, const fp2_t& l0, const fp2
   fp6_t t1 = fp6_mul_1(f.c1, l3);
   fp6_t c1 = fp6_sub(fp6_sub(fp6_mul_01(fp6_add_norm(f.c0, f.c1), l0, fp2_add_norm(l1, l3)), t0), t1);
   fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
-  return fp12_t{c0, c1};
-}
-
-// f * l * l' for two lines l = (a0 + a1 v) + (b1 v) w, l' = (a0' + a1' v) + (b1' v) w
-// (fp12_mul_line's shape).  The lines are multiplied first (6 Fp2 products):
-//   l l' = (C0 + C1 v + C2 v^2) + (D1 v + D2 v^2) w
-//   C0 = a0 a0' + xi b1 b1',  C1 = a0 a1' + a1 a0',  C2 = a1 a1',
-//   D1 = a0 b1' + b1 a0',     D2 = a1 b1' + b1 a1'
-// (each cross sum by Karatsuba over the three diagonal products), then f times that
-// (t0 = f0 C, u = f1 (D1 + D2 v), f1 D = v u): 51 + 18 = 69 Fp products against 78
-// for two fp12_mul_line.
-BGV_MILLER_ATTR fp12_t fp12_mul_lines(const fp12_t& f, const fp2_t& a0, const fp2_t& a1, const fp2_t& b1,
-                                   const fp2_t& a0p, const fp2_t& a1p, const fp2_t& b1p) {
-  const fp2_t m00 = fp2_mul(a0, a0p), m11 = fp2_mul(a1, a1p), mbb = fp2_mul(b1, b1p);
-  fp6_t C;
-  C.c0 = fp2_add(m00, fp2_mul_xi(mbb));
-  C.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a0, a1), fp2_add_norm(a0p, a1p)), m00), m11);
-  C.c2 = m11;
-  const fp2_t D1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a0, b1), fp2_add_norm(a0p, b1p)), m00), mbb);
-  const fp2_t D2 = fp2_sub(fp2_sub(fp2_mul(fp2_add_norm(a1, b1), fp2_add_norm(a1p, b1p)), m11), mbb);
-  const fp6_t t0 = fp6_mul(f.c0, C);
-  const fp6_t t1 = fp6_mul_v(fp6_mul_01(f.c1, D1, D2));  // f1 D
-  const fp6_t CD = fp6_t{C.c0, fp2_add_norm(C.c1, D1), fp2_add_norm(C.c2, D2)};
-  const fp6_t c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_norm(f.c0, f.c1), CD), t0), t1);
-  const fp6_t c0 = fp6_add(t0, fp6_mul_v(t1));
   return fp12_t{c0, c1};
 }
 

@@ -119,58 +119,35 @@ BGV_MILLER_ATTR void miller_add_jq(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, c
   t.z = Z3;
 }
 
-// f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) (conjugated) with one shared accumulator: the
-// squarings of f are paid once for both pairs.  two == false drops the second pair.
-// Q1 (= H(m)) is Jacobian: its additions use miller_add_jq, saving the inversion.
-#ifndef BGV_MILLER_LOOP_ATTR  // bgv_kernels_miller.hip inlines the loop into k_miller
+#ifndef BGV_MILLER_LOOP_ATTR
 #define BGV_MILLER_LOOP_ATTR BGV_NOINLINE
 #endif
-BGV_MILLER_LOOP_ATTR fp12_t miller_loop2(const g1_aff& p1, const g2_jac& q1, const g1_aff& p2, const g2_aff& q2, bool two) {
-  const fp_t xn1 = fp_neg(p1.x), xn2 = fp_neg(p2.x);
-  const miller_jq c1 = miller_jq_make(q1, xn1, p1.y);
-  g2_jac t1 = q1, t2 = jac_from_aff(q2);
-  fp2_t l0, l1, l3, m0, m1, m3;
+
+// The line (l0 + l1 w^2 + l3 w^3) as an Fp12 value (the first step's f = 1 * line).
+BGV_HD fp12_t fp12_from_line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  return fp12_t{fp6_t{l0, l1, fp2_zero()}, fp6_t{fp2_zero(), l3, fp2_zero()}};
+}
+
+// f_{|x|,Q}(P) for ONE pair (conjugated for x < 0): P affine, Q Jacobian (Z != 0).
+// The per-set Miller loop of the blst batch equation (maybeBatch.ts:18-25 ->
+// verifyMultipleAggregateSignatures): e(r_i pk_i, H(m_i)); the signature side
+// e(-G1, sum r_i sig_i) is one team loop per device group (bls_team.h).
+BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_aff& p, const g2_jac& q) {
+  const fp_t xn = fp_neg(p.x);
+  const miller_jq c = miller_jq_make(q, xn, p.y);
+  g2_jac t = q;
+  fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
-  miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
-  fp12_t f = fp12_mul_line(fp12_one(), l0, l1, l3);
-  if (two) {
-    miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
-    f = fp12_mul_line(f, l0, l1, l3);
-  }
-  // -DBGV_MERGE_LINES multiplies both pairs' lines together before they meet f
-  // (fp12_mul_lines: 69 instead of 78 Fp products per step); measured 2-5 % slower
-  // (more live registers), so the lines go into f one by one by default.
-#ifdef BGV_MERGE_LINES
-  const bool merge = two;
-#else
-  const bool merge = false;
-#endif
+  miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+  fp12_t f = fp12_from_line(l0, l1, l3);
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
-      miller_add_jq(t1, &l0, &l1, &l3, c1);
-      if (merge) {
-        miller_add(t2, &m0, &m1, &m3, q2, xn2, p2.y);
-        f = fp12_mul_lines(f, l0, l1, l3, m0, m1, m3);
-      } else {
-        f = fp12_mul_line(f, l0, l1, l3);
-        if (two) {
-          miller_add(t2, &l0, &l1, &l3, q2, xn2, p2.y);
-          f = fp12_mul_line(f, l0, l1, l3);
-        }
-      }
+      miller_add_jq(t, &l0, &l1, &l3, c);
+      f = fp12_mul_line(f, l0, l1, l3);
     }
     f = fp12_sqr(f);
-    miller_dbl(t1, &l0, &l1, &l3, xn1, p1.y);
-    if (merge) {
-      miller_dbl(t2, &m0, &m1, &m3, xn2, p2.y);
-      f = fp12_mul_lines(f, l0, l1, l3, m0, m1, m3);
-    } else {
-      f = fp12_mul_line(f, l0, l1, l3);
-      if (two) {
-        miller_dbl(t2, &l0, &l1, &l3, xn2, p2.y);
-        f = fp12_mul_line(f, l0, l1, l3);
-      }
-    }
+    miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+    f = fp12_mul_line(f, l0, l1, l3);
   }
   return fp12_conj(f);
 }

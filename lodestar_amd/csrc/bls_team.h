@@ -150,6 +150,66 @@ BGV_HD int tm_tower_pos(int c) {
   return (k & 1) * 3 + (k >> 1);
 }
 
+// A Miller-loop line l = l0 + l1 w^2 + l3 w^3 (bls_pairing.h: tower c0.c0, c0.c1, c1.c1).
+// Component c of the line itself (the first step's f = 1 * line).
+BGV_HD fp_t tm_line_lane(int c, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  const int k = c >> 1, e = c & 1;
+  const fp2_t& l = k == 0 ? l0 : (k == 2 ? l1 : l3);
+  const fp_t v = e ? l.c1 : l.c0;
+  return (k == 0 || k == 2 || k == 3) ? v : fp_zero();
+}
+
+// Component c = 2k + e of f * l (A: f's 12 w-basis components; the line's three Fp2
+// coefficients are held by every lane).  c_k = sum_{j in {0,2,3}} f_{k-j} l_j, xi-scaled
+// when k - j wraps below 0: 3 Fp2 terms = 6 double-width products and one reduction
+// (tm_mul_lane's formula per term).  Bounds: 6 products < 48 p^2, columns < 2^63.
+BGV_HD fp_t tm_mul_line_lane(int c, const fp_t* A, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int q = 0; q < 2 * NL; ++q) t[q] = 0;
+  BGV_UNROLL for (int term = 0; term < 3; ++term) {
+    const int j = term == 0 ? 0 : term + 1;  // 0, 2, 3
+    const fp2_t& y = term == 0 ? l0 : (term == 1 ? l1 : l3);
+    const bool wrap = k < j;
+    const int i = wrap ? k - j + 6 : k - j;
+    const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+    const fp_t d = fp_sub_nr(y.c0, y.c1);
+    const fp_t s = fp_add_norm(y.c0, y.c1);
+    const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+    const fp_t X2 = fp_select(e != 0, x1n, x1);
+    const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y.c0, y.c1);
+    const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y.c1, y.c0);
+    wide_mac(t, x0, Y1);
+    wide_mac(t, X2, Y2);
+  }
+  return wide_redc(t);
+}
+
+// f_{|x|,Q}(P), conjugated (x < 0), with f held by a team: the twist point T and the
+// lines are computed by every lane of the team (lane-uniform control flow), the Fp12
+// accumulator is coefficient-parallel (O::sqr, O::mul_line).  P affine, Q Jacobian and
+// finite.  Same steps and lines as miller_loop1 (bls_pairing.h), so the value is equal.
+template <class E, class O>
+BGV_HD E tm_miller_loop(O& o, const g1_aff& p, const g2_jac& q) {
+  const fp_t xn = fp_neg(p.x);
+  const miller_jq cq = miller_jq_make(q, xn, p.y);
+  g2_jac t = q;
+  fp2_t l0, l1, l3;
+  const uint64_t X = BGV_X_ABS;
+  miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+  E f = o.line(l0, l1, l3);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if ((X >> (i + 1)) & 1) {
+      miller_add_jq(t, &l0, &l1, &l3, cq);
+      f = o.mul_line(f, l0, l1, l3);
+    }
+    f = o.sqr(f);
+    miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+    f = o.mul_line(f, l0, l1, l3);
+  }
+  return o.conj(f);
+}
+
 // The hard-part x-chain on representatives modulo Fp6* (see the header).  O supplies
 // mul, sqr, conj, frob, frob2, is_fp6 on its element type E.
 template <class O, class E>
@@ -190,6 +250,21 @@ struct tm_emu_ops {
   BGV_HD tm_emu_t sqr(const tm_emu_t& a) {
     tm_emu_t r;
     for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_sqr_lane(c, a.c);
+    return r;
+  }
+  BGV_HD tm_emu_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_line_lane(c, l0, l1, l3);
+    return r;
+  }
+  BGV_HD tm_emu_t mul_line(const tm_emu_t& a, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = tm_mul_line_lane(c, a.c, l0, l1, l3);
+    return r;
+  }
+  BGV_HD tm_emu_t one() {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) r.c[c] = c == 0 ? fp_one() : fp_zero();
     return r;
   }
   BGV_HD tm_emu_t conj(const tm_emu_t& a) {

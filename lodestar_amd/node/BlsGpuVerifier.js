@@ -115,7 +115,10 @@ class BlsGpuVerifier {
     return results.every((v) => v === true);
   }
 
+  // index.ts:176-197.  Idempotent; device calls already in flight complete (the library
+  // drains them before releasing the context), queued and later jobs reject QUEUE_ABORTED.
   async close() {
+    if (this.closed) return;
     if (this.bufferedJobs) clearTimeout(this.bufferedJobs.timeout);
     const pending = this.jobs.concat(this.bufferedJobs ? this.bufferedJobs.jobs : []);
     for (const job of pending) job.reject(new QueueError("QUEUE_ABORTED"));
@@ -256,4 +259,4 @@ function unwrap(code) {
   return code === 1;
 }
 
-module.exports = {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, getAggregatedPubkeysCount, addon};
+module.exports = {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, getAggregatedPubkeysCount, toNativeSet, addon};

@@ -3,8 +3,15 @@
  *
  * Exposes the C-ABI (include/blsgpu.h) to JavaScript; BlsGpuVerifier.js builds the
  * IBlsVerifier (packages/beacon-node/src/chain/bls/interface.ts:20-46) on top.
- * Verification runs in napi_async_work on the libuv pool and resolves a Promise on
- * the main thread, like the reference's worker round trip (multithread/index.ts:290-381).
+ * Verification goes through bgv_verify_async: the library's dispatcher threads run it and
+ * hand the completion to the main thread through a napi_threadsafe_function, which
+ * resolves the Promise, like the reference's worker round trip
+ * (multithread/index.ts:290-381).  No libuv pool thread is held while a batch runs.
+ *
+ * Lifetime: the ctx value is an external over a small wrapper.  close(ctx) is idempotent:
+ * it closes the library context (queued and in-flight verifies complete first, later
+ * calls reject with QUEUE_ABORTED) but does not free it; the memory is released by the
+ * external's finalizer, which cannot run while a verify holds a reference to the ctx.
  *
  *   init(devices?: number[]) -> ctx
  *   pubkeysPut(ctx, firstIndex, keys: Uint8Array, fmt: 48 | 96)
@@ -41,11 +48,30 @@ static napi_value throw_code(napi_env env, int rc) {
   return NULL;
 }
 
-static bgv_ctx* get_ctx(napi_env env, napi_value v) {
+typedef struct {
+  bgv_ctx* c;
+  int closed;                    /* close() was called: every entry point rejects */
+  uint32_t inflight;             /* async verifies not yet completed */
+  napi_threadsafe_function tsfn; /* completions from the dispatcher threads */
+} addon_ctx;
+
+static addon_ctx* get_actx(napi_env env, napi_value v) {
   void* p = NULL;
   if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
-  return (bgv_ctx*)p;
+  return (addon_ctx*)p;
 }
+
+/* the library context of an open addon context, else NULL (the caller throws) */
+static bgv_ctx* get_ctx(napi_env env, napi_value v) {
+  addon_ctx* a = get_actx(env, v);
+  return a && !a->closed ? a->c : NULL;
+}
+
+#define OPEN_CTX(env, v, ctx)                                 \
+  bgv_ctx* ctx = get_ctx((env), (v));                         \
+  do {                                                        \
+    if (!ctx) return throw_code((env), -BGV_E_CLOSED);        \
+  } while (0)
 
 static int get_bytes(napi_env env, napi_value v, uint8_t** data, size_t* len) {
   napi_typedarray_type t;
@@ -65,6 +91,25 @@ static int get_bytes(napi_env env, napi_value v, uint8_t** data, size_t* len) {
   }
   return -1;
 }
+
+typedef struct {
+  addon_ctx* actx;
+  napi_ref ctx_ref; /* keeps the ctx external (and its finalizer) alive */
+  bgv_job* jobs;
+  size_t njobs;
+  bgv_set* sets;
+  size_t nsets;
+  int mode;
+  int32_t* codes;
+  bgv_stats stats;
+  int rc;
+  napi_deferred deferred;
+  napi_ref* refs; /* keep every input buffer alive until completion */
+  size_t nrefs;
+} verify_req;
+
+static void verify_call_js(napi_env env, napi_value js_cb, void* context, void* data);
+static void addon_finalize(napi_env env, void* data, void* hint);
 
 static napi_value js_init(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -88,17 +133,33 @@ static napi_value js_init(napi_env env, napi_callback_info info) {
   bgv_ctx* ctx = NULL;
   int rc = bgv_init(ndev ? devs : NULL, ndev, &ctx);
   if (rc) return throw_code(env, rc);
-  napi_value out;
-  CHECK(env, napi_create_external(env, ctx, NULL, NULL, &out));
+  addon_ctx* a = (addon_ctx*)calloc(1, sizeof(addon_ctx));
+  a->c = ctx;
+  napi_value out, name;
+  if (napi_create_string_utf8(env, "blsgpu.verify.done", NAPI_AUTO_LENGTH, &name) != napi_ok ||
+      napi_create_threadsafe_function(env, NULL, NULL, name, 0, 1, NULL, NULL, NULL, verify_call_js, &a->tsfn) !=
+          napi_ok ||
+      napi_unref_threadsafe_function(env, a->tsfn) != napi_ok ||
+      napi_create_external(env, a, addon_finalize, NULL, &out) != napi_ok) {
+    bgv_destroy(ctx);
+    free(a);
+    napi_throw_error(env, NULL, "blsgpu: N-API failure");
+    return NULL;
+  }
   return out;
 }
 
+/* close(ctx): idempotent; the library drains queued and in-flight verifies (their
+ * completions still resolve), and every later call rejects with QUEUE_ABORTED. */
 static napi_value js_close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
-  if (ctx) bgv_destroy(ctx);
+  addon_ctx* a = get_actx(env, argv[0]);
+  if (a && !a->closed) {
+    a->closed = 1;
+    bgv_close(a->c);
+  }
   return NULL;
 }
 
@@ -116,7 +177,7 @@ static napi_value js_pubkeys_put(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint32_t first = 0;
   int32_t fmt = 48;
   uint8_t* keys;
@@ -133,7 +194,7 @@ static napi_value js_keygen(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3], ab, out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t* sks;
   size_t len;
   int64_t first = -1;
@@ -151,7 +212,7 @@ static napi_value js_sign(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3], ab, out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t *sks, *msgs;
   size_t l1, l2;
   if (get_bytes(env, argv[1], &sks, &l1) || get_bytes(env, argv[2], &msgs, &l2) || l1 != l2)
@@ -188,7 +249,7 @@ static napi_value js_aggregate_pubkeys(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t* idx;
   size_t len;
   if (get_bytes(env, argv[1], &idx, &len) || len % 4) return throw_code(env, -BGV_E_ARG);
@@ -205,7 +266,7 @@ static napi_value js_hash_to_g2(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t* msg;
   size_t len;
   if (get_bytes(env, argv[1], &msg, &len)) return throw_code(env, -BGV_E_ARG);
@@ -225,7 +286,7 @@ static napi_value js_pubkeys_validate(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t* keys;
   size_t len;
   if (get_bytes(env, argv[1], &keys, &len) || len % 48) return throw_code(env, -BGV_E_ARG);
@@ -257,7 +318,7 @@ static napi_value js_aggregate_signatures(napi_env env, napi_callback_info info)
   size_t argc = 2;
   napi_value argv[2];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint32_t naggs = 0;
   if (napi_get_array_length(env, argv[1], &naggs) != napi_ok) return throw_code(env, -BGV_E_ARG);
   uint32_t* counts = (uint32_t*)calloc(naggs ? naggs : 1, sizeof(uint32_t));
@@ -315,7 +376,7 @@ static napi_value js_deposits_verify(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bgv_ctx* ctx = get_ctx(env, argv[0]);
+  OPEN_CTX(env, argv[0], ctx);
   uint8_t *keys, *msgs, *sigs;
   size_t lk, lm, ls;
   if (get_bytes(env, argv[1], &keys, &lk) || get_bytes(env, argv[2], &msgs, &lm) ||
@@ -330,62 +391,10 @@ static napi_value js_deposits_verify(napi_env env, napi_callback_info info) {
   return out;
 }
 
-/* ---- verify: napi_async_work + Promise ---------------------------------- */
-typedef struct {
-  bgv_ctx* ctx;
-  bgv_job* jobs;
-  size_t njobs;
-  bgv_set* sets;
-  size_t nsets;
-  int mode;
-  int32_t* codes;
-  bgv_stats stats;
-  int rc;
-  napi_deferred deferred;
-  napi_async_work work;
-  napi_ref* refs; /* keep every input buffer alive until completion */
-  size_t nrefs;
-} verify_req;
-
-static void verify_execute(napi_env env, void* data) {
-  (void)env;
-  verify_req* r = (verify_req*)data;
-  r->rc = bgv_verify(r->ctx, r->jobs, r->njobs, r->sets, r->nsets, r->mode, r->codes, &r->stats);
-}
-
-static void verify_complete(napi_env env, napi_status status, void* data) {
-  verify_req* r = (verify_req*)data;
-  if (status != napi_ok || r->rc) {
-    napi_value err, msg;
-    napi_create_string_utf8(env, bgv_strerror(r->rc ? r->rc : -BGV_E_DEVICE), NAPI_AUTO_LENGTH, &msg);
-    napi_create_error(env, NULL, msg, &err);
-    napi_reject_deferred(env, r->deferred, err);
-  } else {
-    napi_value ab, arr;
-    void* dst;
-    napi_create_arraybuffer(env, 4 * r->njobs, &dst, &ab);
-    memcpy(dst, r->codes, 4 * r->njobs);
-    napi_create_typedarray(env, napi_int32_array, r->njobs, ab, 0, &arr);
-    /* codes.stats: the call's BlsWorkResult-style counters (multithread/types.ts:24-36) */
-    napi_value st, v;
-    napi_create_object(env, &st);
-    napi_create_double(env, (double)r->stats.batch_retries, &v);
-    napi_set_named_property(env, st, "batchRetries", v);
-    napi_create_double(env, (double)r->stats.batch_sigs_success, &v);
-    napi_set_named_property(env, st, "batchSigsSuccess", v);
-    napi_create_double(env, (double)r->stats.device_groups, &v);
-    napi_set_named_property(env, st, "deviceGroups", v);
-    napi_create_double(env, (double)r->stats.sets_verified, &v);
-    napi_set_named_property(env, st, "setsVerified", v);
-    napi_create_double(env, r->stats.device_ms, &v);
-    napi_set_named_property(env, st, "deviceMs", v);
-    napi_create_double(env, r->stats.wall_ms, &v);
-    napi_set_named_property(env, st, "wallMs", v);
-    napi_set_named_property(env, arr, "stats", st);
-    napi_resolve_deferred(env, r->deferred, arr);
-  }
+/* ---- verify: bgv_verify_async + threadsafe completion + Promise ----------- */
+static void free_req(napi_env env, verify_req* r) {
   for (size_t i = 0; i < r->nrefs; ++i) napi_delete_reference(env, r->refs[i]);
-  napi_delete_async_work(env, r->work);
+  if (r->ctx_ref) napi_delete_reference(env, r->ctx_ref);
   free(r->refs);
   free(r->jobs);
   free(r->sets);
@@ -393,12 +402,77 @@ static void verify_complete(napi_env env, napi_status status, void* data) {
   free(r);
 }
 
+static void settle(napi_env env, verify_req* r) {
+  if (r->rc) {
+    napi_value err, msg;
+    napi_create_string_utf8(env, bgv_strerror(r->rc), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, r->deferred, err);
+    return;
+  }
+  napi_value ab, arr;
+  void* dst;
+  napi_create_arraybuffer(env, 4 * r->njobs, &dst, &ab);
+  memcpy(dst, r->codes, 4 * r->njobs);
+  napi_create_typedarray(env, napi_int32_array, r->njobs, ab, 0, &arr);
+  /* codes.stats: the call's BlsWorkResult-style counters (multithread/types.ts:24-36) */
+  napi_value st, v;
+  napi_create_object(env, &st);
+  napi_create_double(env, (double)r->stats.batch_retries, &v);
+  napi_set_named_property(env, st, "batchRetries", v);
+  napi_create_double(env, (double)r->stats.batch_sigs_success, &v);
+  napi_set_named_property(env, st, "batchSigsSuccess", v);
+  napi_create_double(env, (double)r->stats.device_groups, &v);
+  napi_set_named_property(env, st, "deviceGroups", v);
+  napi_create_double(env, (double)r->stats.sets_verified, &v);
+  napi_set_named_property(env, st, "setsVerified", v);
+  napi_create_double(env, r->stats.device_ms, &v);
+  napi_set_named_property(env, st, "deviceMs", v);
+  napi_create_double(env, r->stats.wall_ms, &v);
+  napi_set_named_property(env, st, "wallMs", v);
+  napi_set_named_property(env, arr, "stats", st);
+  napi_resolve_deferred(env, r->deferred, arr);
+}
+
+/* main thread: a verify finished on a dispatcher thread */
+static void verify_call_js(napi_env env, napi_value js_cb, void* context, void* data) {
+  (void)js_cb;
+  (void)context;
+  verify_req* r = (verify_req*)data;
+  if (env) {
+    addon_ctx* a = r->actx;
+    settle(env, r);
+    if (--a->inflight == 0) napi_unref_threadsafe_function(env, a->tsfn);
+    free_req(env, r);
+  }
+}
+
+/* dispatcher thread (library): codes and stats are filled; hop to the main thread */
+static void verify_done(void* user, int rc) {
+  verify_req* r = (verify_req*)user;
+  r->rc = rc;
+  napi_call_threadsafe_function(r->actx->tsfn, r, napi_tsfn_nonblocking);
+}
+
+/* the ctx external was collected: no verify references it any more */
+static void addon_finalize(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  addon_ctx* a = (addon_ctx*)data;
+  if (!a) return;
+  napi_release_threadsafe_function(a->tsfn, napi_tsfn_abort);
+  bgv_destroy(a->c);  /* bgv_close first when close() was never called */
+  free(a);
+}
+
 static napi_value js_verify(napi_env env, napi_callback_info info) {
   size_t argc = 3;
   napi_value argv[3];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  addon_ctx* a = get_actx(env, argv[0]);
+  if (!a || a->closed) return throw_code(env, -BGV_E_CLOSED);
   verify_req* r = (verify_req*)calloc(1, sizeof(verify_req));
-  r->ctx = get_ctx(env, argv[0]);
+  r->actx = a;
   int32_t mode = 0;
   if (argc >= 3) napi_get_value_int32(env, argv[2], &mode);
   r->mode = mode;
@@ -446,12 +520,7 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
       size_t pkl, ml, sl;
       if (get_bytes(env, pk, &pkd, &pkl) || get_bytes(env, msg, &md, &ml) || get_bytes(env, sig, &sd, &sl) ||
           ml != 32 || (!by_index && pkl % 96)) {
-        for (size_t i = 0; i < r->nrefs; ++i) napi_delete_reference(env, r->refs[i]);
-        free(r->refs);
-        free(r->jobs);
-        free(r->sets);
-        free(r->codes);
-        free(r);
+        free_req(env, r);
         return throw_code(env, -BGV_E_ARG);
       }
       if (by_index) {
@@ -469,11 +538,18 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
       napi_create_reference(env, sig, 1, &r->refs[r->nrefs++]);
     }
   }
-  napi_value promise, name;
+  napi_value promise;
   CHECK(env, napi_create_promise(env, &r->deferred, &promise));
-  CHECK(env, napi_create_string_utf8(env, "blsgpu.verify", NAPI_AUTO_LENGTH, &name));
-  CHECK(env, napi_create_async_work(env, NULL, name, verify_execute, verify_complete, r, &r->work));
-  CHECK(env, napi_queue_async_work(env, r->work));
+  /* the ctx external stays alive (no finalizer) until this request completes */
+  CHECK(env, napi_create_reference(env, argv[0], 1, &r->ctx_ref));
+  if (a->inflight++ == 0) napi_ref_threadsafe_function(env, a->tsfn);
+  int rc = bgv_verify_async(a->c, r->jobs, r->njobs, r->sets, r->nsets, r->mode, r->codes, &r->stats, verify_done, r);
+  if (rc) { /* rejected before queueing (closed, bad arguments): settle now */
+    r->rc = rc;
+    settle(env, r);
+    if (--a->inflight == 0) napi_unref_threadsafe_function(env, a->tsfn);
+    free_req(env, r);
+  }
   return promise;
 }
 

@@ -465,26 +465,35 @@ def g1_decompress(b: bytes):
         raise BlstError(BLST_POINT_NOT_ON_CURVE)
     if fp_lex_largest(y) != bool(flags & 0x20):
         y = (-y) % P
+    if x == 0:  # (0, +-2): on the curve, order 3 (blst POINTonE1_Uncompress_Z)
+        raise BlstError(BLST_POINT_NOT_IN_GROUP)
     return (x, y)
 
 
 def g1_deserialize(b: bytes):
-    """96-byte uncompressed G1, no subgroup check (worker.ts:112 trusts pubkeys)."""
+    """96-byte G1 record, no subgroup check (worker.ts:112 trusts pubkeys), decoded as
+    blst's POINTonE1_Deserialize_Z does for PublicKey.fromBytes of 96 bytes:
+    top bits 000 -> big-endian x || y; 0x80 -> the first 48 bytes compressed;
+    0x40 alone -> infinity iff all other bits are zero; otherwise BAD_ENCODING."""
     if len(b) != 96:
         raise BlstError(BLST_INVALID_SIZE)
     if b[0] & 0x80:
-        raise BlstError(BLST_BAD_ENCODING)
+        return g1_decompress(bytes(b[:48]))
     if b[0] & 0x40:
         if (b[0] & 0x3F) == 0 and not any(b[1:]):
             return None
         raise BlstError(BLST_BAD_ENCODING)
-    x = int.from_bytes(bytes([b[0] & 0x1F]) + b[1:48], "big")
+    if b[0] & 0x20:
+        raise BlstError(BLST_BAD_ENCODING)
+    x = int.from_bytes(b[:48], "big")
     y = int.from_bytes(b[48:], "big")
     if x >= P or y >= P:
         raise BlstError(BLST_BAD_ENCODING)
     pt = (x, y)
     if not g1_on_curve(pt):
         raise BlstError(BLST_POINT_NOT_ON_CURVE)
+    if x == 0:
+        raise BlstError(BLST_POINT_NOT_IN_GROUP)
     return pt
 
 

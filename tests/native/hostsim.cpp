@@ -39,23 +39,6 @@ static void out_g1(uint8_t* be, const g1_aff& a) {
   out_fp(be + 48, a.y);
 }
 
-// host copy of the device's fixed-base table (k_gtab_build), built on first use
-static const g1_aff* host_gtab() {
-  static g1_aff* tab = nullptr;
-  if (!tab) {
-#ifdef BGV_COUNT_OPS
-    const unsigned long long m = bgv_count_mul, q = bgv_count_sqr;
-#endif
-    tab = new g1_aff[BGV_GTAB_ENTRIES];
-    for (int i = 0; i < BGV_GTAB_ENTRIES; ++i) tab[i] = g1_gtab_entry(i);
-#ifdef BGV_COUNT_OPS
-    bgv_count_mul = m;  // one-time table build is not per-set work
-    bgv_count_sqr = q;
-#endif
-  }
-  return tab;
-}
-
 extern "C" {
 #ifdef BGV_COUNT_OPS
 unsigned long long bgv_count_mul = 0, bgv_count_sqr = 0;
@@ -63,25 +46,29 @@ void hs_count_reset() { bgv_count_mul = bgv_count_sqr = 0; }
 unsigned long long hs_count_mul() { return bgv_count_mul; }
 unsigned long long hs_count_sqr() { return bgv_count_sqr; }
 // per-lane bodies of the verify kernels (bgv_kernels.hip), for counting only
-int hs_k_sig_body(const uint8_t* sig96) {
+int hs_k_sig_body(const uint8_t* sig96, uint64_t r) {
   g2_aff a;
   bool inf;
   if (g2_decompress(&a, &inf, sig96) || inf) return 0;
-  return g2_in_subgroup(jac_from_aff(a));
+  if (!g2_in_subgroup(jac_from_aff(a))) return 0;
+  return !jac_is_inf(jac_mul_u64(jac_from_aff(a), r));  // r * sig for the group sum
 }
 int hs_k_hash_body(const uint8_t* msg32) { return !jac_is_inf(hash_to_g2(msg32, 32)); }
 int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_aff p = in_g1(pk_aff_tl);
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
-  const g1_jac a = jac_mul_u64(acc, r);
-  const g1_jac g = g1_neg_gen_mul(host_gtab(), r);
-  g1_aff pa, ga;
-  jac2_to_aff(&pa, &ga, a, g);
-  return 1;
+  g1_aff pa;
+  return jac_to_aff(&pa, jac_mul_u64(acc, r));
 }
 void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
-  (void)miller_loop2(in_g1(p), jac_from_aff(in_g2(q)), g1_neg_generator(), in_g2(q), true);
+  (void)miller_loop1(in_g1(p), jac_from_aff(in_g2(q)));
+}
+// the group's signature pair e(-G1, sum r_i sig_i), counted as the one-lane loop
+void hs_k_group_miller_body(const uint8_t* q) { (void)miller_loop1(g1_neg_generator(), jac_from_aff(in_g2(q))); }
+// one complete G2 addition of the group's signature sum
+void hs_k_group_add_body(const uint8_t* q, const uint8_t* q2) {
+  (void)jac_add(jac_from_aff(in_g2(q)), jac_from_aff(in_g2(q2)));
 }
 void hs_k_final_body(const uint8_t* f) { (void)fp12_is_one(final_exp(in_fp12(f))); }
 // one Fp12 product of the group product in k_final (operands already in Montgomery form)
@@ -123,11 +110,6 @@ void hs_fp12_cyc_sqr(uint8_t* r, const uint8_t* a) { out_fp12(r, fp12_cyclotomic
 void hs_fp12_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   out_fp12(r, fp12_mul_line(in_fp12(f), in_fp2(l0), in_fp2(l1), in_fp2(l3)));
 }
-void hs_fp12_mul_lines(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3,
-                       const uint8_t* m0, const uint8_t* m1, const uint8_t* m3) {
-  out_fp12(r, fp12_mul_lines(in_fp12(f), in_fp2(l0), in_fp2(l1), in_fp2(l3), in_fp2(m0), in_fp2(m1), in_fp2(m3)));
-}
-
 // G2 compressed (96 B) -> test-layout affine (192 B); returns BGV code, 100 = infinity
 int hs_g2_decompress(uint8_t* out, const uint8_t* in) {
   g2_aff a;
@@ -166,8 +148,6 @@ int hs_g2_psi(uint8_t* out, const uint8_t* a) { return g2_out(out, g2_psi(jac_fr
 int hs_g2_clear_cofactor(uint8_t* out, const uint8_t* a) {
   return g2_out(out, g2_clear_cofactor(jac_from_aff(in_g2(a))));
 }
-// r * (-G1) via the fixed-base table (task_pk)
-int hs_g1_neg_gen_mul(uint8_t* out, uint64_t r) { return g1_out(out, g1_neg_gen_mul(host_gtab(), r)); }
 int hs_g1_mul_u64(uint8_t* out, const uint8_t* aff, uint64_t k) {
   return g1_out(out, jac_mul_u64(jac_from_aff(in_g1(aff)), k));
 }
@@ -202,15 +182,6 @@ int hs_hash_to_g2(uint8_t* out_aff, uint8_t* out_comp96, const uint8_t* msg, uin
 // P (test layout g1) , Q (test layout g2) -> Miller loop value and pairing^3
 void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12(out, miller_loop(in_g1(p), in_g2(q))); }
 void hs_final_exp(uint8_t* out, const uint8_t* f) { out_fp12(out, final_exp(in_fp12(f))); }
-void hs_miller_loop2(uint8_t* out, const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2,
-                     int two) {
-  // Q1 handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
-  const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};
-  const g2_aff a = in_g2(q1);
-  const fp2_t l2 = fp2_sqr(l);
-  const g2_jac q1j = {fp2_mul(a.x, l2), fp2_mul(a.y, fp2_mul(l2, l)), l};
-  out_fp12(out, miller_loop2(in_g1(p1), q1j, in_g1(p2), in_g2(q2), two != 0));
-}
 // team-parallel closing arithmetic (bls_team.h), emulated lane by lane
 void hs_team_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {
   tm_emu_ops o;
@@ -237,14 +208,34 @@ int hs_team_final_is_one(const uint8_t* f) {
   return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
 }
 int hs_final_is_one(const uint8_t* f) { return fp12_is_one(final_exp(in_fp12(f))); }
-// per-set path of k_prep's pk task + k_miller for one single set: r pk, r (-G1) via the
-// shared-inversion affine conversion, then the 2-pair loop and the final exponentiation
+// Q handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
+static g2_jac jac_scaled(const g2_aff& a) {
+  const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};
+  const fp2_t l2 = fp2_sqr(l);
+  return g2_jac{fp2_mul(a.x, l2), fp2_mul(a.y, fp2_mul(l2, l)), l};
+}
+void hs_miller_loop1(uint8_t* out, const uint8_t* p, const uint8_t* q) {
+  out_fp12(out, miller_loop1(in_g1(p), jac_scaled(in_g2(q))));
+}
+// the team Miller loop of k_final (bls_team.h tm_miller_loop), emulated lane by lane
+void hs_team_miller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
+  tm_emu_ops o;
+  out_fp12(out, tm_emu_to_fp12(tm_miller_loop<tm_emu_t>(o, in_g1(p), jac_scaled(in_g2(q)))));
+}
+void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
+  tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul_line(tm_emu_from_fp12(in_fp12(f)), in_fp2(l0), in_fp2(l1), in_fp2(l3))));
+}
+// one set through the device equation: k_prep (r pk affine, r sig Jacobian), k_miller
+// (e(r pk, H)), the group's team loop e(-G1, r sig), the product and the team final check
 int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* sig_aff, uint64_t r) {
-  const g1_jac a = jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r);
-  const g1_jac g = jac_mul_u64(jac_from_aff(g1_neg_generator()), r);
-  g1_aff pa, ga;
-  jac2_to_aff(&pa, &ga, a, g);
-  return fp12_is_one(final_exp(miller_loop2(pa, jac_from_aff(in_g2(h_aff)), ga, in_g2(sig_aff), true)));
+  g1_aff pa;
+  if (!jac_to_aff(&pa, jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r))) return 0;
+  const g2_jac rs = jac_mul_u64(jac_from_aff(in_g2(sig_aff)), r);
+  tm_emu_ops o;
+  const tm_emu_t f = tm_emu_from_fp12(miller_loop1(pa, jac_from_aff(in_g2(h_aff))));
+  const tm_emu_t g = tm_miller_loop<tm_emu_t>(o, g1_neg_generator(), rs);
+  return tm_final_exp_is_one(o, o.mul(f, g));
 }
 
 int hs_g1_decompress(uint8_t* out, const uint8_t* in48) {

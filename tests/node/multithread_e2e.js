@@ -4,7 +4,7 @@
 // Usage: node tests/node/multithread_e2e.js [cpu]   (cpu: load/export checks only, no device)
 const assert = require("assert");
 const path = require("path");
-const {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, addon} = require(
+const {BlsGpuVerifier, SignatureSetType, QueueError, chunkifyMaximizeChunkSize, addon, toNativeSet: toNative} = require(
   path.join(__dirname, "..", "..", "lodestar_amd", "node", "BlsGpuVerifier.js")
 );
 
@@ -204,6 +204,22 @@ async function gpuChecks() {
   await pool.close();
   await assert.rejects(pending, (e) => e instanceof QueueError && e.type.code === "QUEUE_ABORTED");
   await assert.rejects(pool.verifySignatureSets(sets), (e) => e instanceof QueueError);
+  await pool.close(); // idempotent
+  // close() while device calls are in flight (ADVICE r01: the context must outlive them):
+  // calls already handed to the library complete with their verdicts, later ones reject,
+  // a second close is a no-op, and addon entry points on the closed ctx throw QUEUE_ABORTED
+  const pool2 = newPool();
+  const inflight = [];
+  for (let i = 0; i < 16; i++) inflight.push(addon.verify(pool2.ctx, [{sets: sets.map(toNative), batchable: true}], 0));
+  const ctx2 = pool2.ctx;
+  await pool2.close();
+  await pool2.close();
+  const codes = await Promise.all(inflight);
+  for (const c of codes) assert.deepStrictEqual(Array.from(c), [1]);
+  await assert.rejects(addon.verify(ctx2, [{sets: sets.map(toNative), batchable: true}], 0), /QUEUE_ABORTED/);
+  assert.throws(() => addon.aggregatePubkeys(ctx2, Uint32Array.from([0])), /QUEUE_ABORTED/);
+  assert.throws(() => addon.hashToG2(ctx2, new Uint8Array(32)), /QUEUE_ABORTED/);
+  addon.close(ctx2);
   report.close = "ok";
   return report;
 }

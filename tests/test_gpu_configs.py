@@ -111,6 +111,66 @@ def test_config4_gossip_8192(big):
     assert c.verify_jobs([(sets, True)], native.MODE_WORKER) == [-1]
 
 
+def _block_import_sets(c, sks, att_size=128):
+    """config 3 as chain/blocks/verifyBlocksSignatures.ts:34 sends it: randao (single),
+    128 aggregate attestations of att_size distinct validators, one 512-key sync-committee
+    aggregate and the proposer (single); aggregate signatures sign with the summed key."""
+    import hashlib as _h
+    from lodestar_amd import native
+    groups = [[7]] + [list(range(att_size * a, att_size * a + att_size)) for a in range(128)]
+    groups += [list(range(600000, 600000 + 512)), [11]]
+    msgs = [_h.sha256(b"block-import-%d" % i).digest() for i in range(len(groups))]
+    agg = [sum(sks[k] for k in g) % R for g in groups]
+    sigs = c.sign(b"".join(sk_bytes(k) for k in agg), b"".join(msgs))
+    return [native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=g) for i, g in enumerate(groups)], groups
+
+
+def test_config3_block_import_full_shape(big):
+    """One non-batchable call of 131 sets (16,898 pubkeys aggregated on the device); a
+    corrupted attestation signature, a sync aggregate missing a member and a bad encoding
+    each turn the call false / reject, as the reference's single job does (no retry)."""
+    from lodestar_amd import native
+    c, sks = big
+    sets, groups = _block_import_sets(c, sks)
+    assert len(sets) == 131 and sum(len(g) for g in groups) == 16898
+    assert c.verify_jobs([(sets, False)], native.MODE_WORKER) == [1]
+    assert c.verify_jobs([(sets, False)], native.MODE_PER_JOB) == [1]
+    bad = list(sets)
+    bad[40] = native.SetSpec(sets[40].msg, sets[41].sig, pk_indices=groups[40])  # another attestation's sig
+    assert c.verify_jobs([(bad, False)], native.MODE_WORKER) == [0]
+    bad = list(sets)
+    bad[129] = native.SetSpec(sets[129].msg, sets[129].sig, pk_indices=groups[129][:-1])  # sync member missing
+    assert c.verify_jobs([(bad, False)], native.MODE_WORKER) == [0]
+    bad = list(sets)
+    bad[3] = native.SetSpec(sets[3].msg, bytes([sets[3].sig[0] & 0x7F]) + sets[3].sig[1:], pk_indices=groups[3])
+    assert c.verify_jobs([(bad, False)], native.MODE_WORKER) == [-native.BLST_BAD_ENCODING]
+    # the 512-key attestation variant of SURVEY 8(d) config 3
+    sets512, _ = _block_import_sets(c, sks, att_size=512)
+    assert c.verify_jobs([(sets512, False)], native.MODE_WORKER) == [1]
+
+
+def test_config5_aggregate_variant_2048x512(big):
+    """Config 5's aggregate variant: 2048 aggregates of 512 validators (the whole 2^20-key
+    cache), chunked into 128-set batchable jobs as the pool does (index.ts:155-166); one
+    aggregate signed over a wrong root fails its job alone."""
+    from lodestar_amd import native
+    c, sks = big
+    n, size = 2048, 512
+    roots = [hashlib.sha256(b"config5-agg-%d" % q).digest() for q in range(n)]
+    agg = [sum(sks[size * q:size * q + size]) % R for q in range(n)]
+    sigs = c.sign(b"".join(sk_bytes(k) for k in agg), b"".join(roots))
+    sets = [native.SetSpec(roots[q], sigs[96 * q:96 * q + 96], pk_indices=range(size * q, size * q + size))
+            for q in range(n)]
+    jobs = [(sets[j:j + 128], True) for j in range(0, n, 128)]
+    assert c.verify_jobs(jobs, native.MODE_WORKER) == [1] * 16
+    q = 1500
+    sets[q] = native.SetSpec(roots[q - 1], sets[q].sig, pk_indices=range(size * q, size * q + size))
+    jobs = [(sets[j:j + 128], True) for j in range(0, n, 128)]
+    want = [1] * 16
+    want[q // 128] = 0
+    assert c.verify_jobs(jobs, native.MODE_WORKER) == want
+
+
 def test_config5_shard_of_epoch_sweep(big):
     """Rank 0's 131,072 of 1,048,576 sets over the full 2^20-key cache (indices spread
     over all of it), 1 % corrupted; verdicts by construction."""
