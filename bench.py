@@ -26,6 +26,7 @@ The JSON line carries:
 import argparse
 import hashlib
 import json
+import math
 import os
 import random
 import statistics
@@ -224,6 +225,95 @@ def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
                       % (passes, nsample, threads, dt, nverified / dt / threads)}
 
 
+def super_batch_calls(steps, nsets, dispatchers=2, max_slots=163840):
+    """Calls per super-batch: the largest b with b * nsets <= max_slots dividing the timed
+    step count into a multiple of `dispatchers` super-batches.  The library keeps one
+    super-batch in flight per dispatcher, so completions repeat with a period of
+    `dispatchers` batches: a window of whole periods measures the steady-state rate."""
+    best = 1
+    for b in range(1, max(1, max_slots // nsets) + 1):
+        if steps % b == 0 and (steps // b) % dispatchers == 0:
+            best = b
+    return best
+
+
+def stream_window(step, expect, warmup, steps, inflight):
+    """Calls stream continuously, `inflight` outstanding (the pool's concurrent jobs).  The
+    timed window runs from the warmup-th completion to the (warmup + steps)-th completion,
+    so exactly `steps` calls (steps x nsets sets) complete inside it, with the device busy
+    on both sides of it; feeding stops once the window is complete and the calls still in
+    flight drain untimed."""
+    import threading
+    lock = threading.Lock()
+    st = {"submitted": 0, "limit": None}
+    done, errors = [], []
+    target = warmup + steps
+
+    def worker():
+        while True:
+            with lock:
+                if st["limit"] is not None and st["submitted"] >= st["limit"]:
+                    return
+                st["submitted"] += 1
+            ts = time.perf_counter()
+            try:
+                got, s = step()
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(e)
+                with lock:
+                    st["limit"] = st["submitted"]
+                return
+            t = time.perf_counter()
+            with lock:
+                done.append((t, t - ts, s, got == expect))
+                if len(done) >= target and st["limit"] is None:
+                    st["limit"] = st["submitted"]
+
+    t_begin = time.perf_counter()
+    threads = [threading.Thread(target=worker, daemon=True) for _ in range(inflight)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    done.sort(key=lambda d: d[0])
+    if len(done) < target or not all(d[3] for d in done):
+        raise SystemExit("verdict mismatch")
+    t0 = done[warmup - 1][0] if warmup else t_begin
+    window = done[warmup:target]
+    return {"elapsed": window[-1][0] - t0, "latencies": [d[1] for d in window], "stats": [d[2] for d in window],
+            "calls_total": len(done)}
+
+
+ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
+
+
+def roofline_isolated(ctx, native, nkeys):
+    """The dominant kernel measured alone at full occupancy: one verify call of ROOF_SETS
+    valid one-set jobs (every other stream idle), per-kernel HIP events on the launching
+    stream.  k_miller: ROOF_SETS + 1008 lanes = 1024 waves of one wave per SIMD."""
+    n = ROOF_SETS
+    key_of = [(i * 7919) % nkeys for i in range(n)]
+    msgs = [hashlib.sha256(b"lodestar-roof" + i.to_bytes(4, "little")).digest() for i in range(n)]
+    sigs = ctx.sign(b"".join(interop_sk(k) for k in key_of), b"".join(msgs))
+    jobs = [([native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=[key_of[i]])], True) for i in range(n)]
+    packed = native.PackedCall(jobs)
+    out = (native.ctypes.c_int32 * n)()
+    ms = {}
+    for rep in range(3):
+        ctx.profile(1)
+        rc = ctx.lib.bgv_verify(ctx.handle, packed.jobs, n, packed.sets, packed.nsets, native.MODE_WORKER, out, None)
+        if rc != 0 or any(v != 1 for v in out):
+            raise SystemExit("roofline call: verdict mismatch")
+        k, launches = ctx.profile(0)
+        assert launches == 1
+        if rep:  # first call warms up
+            for name, v in k.items():
+                ms.setdefault(name, []).append(v)
+    return {"sets": n, "kernel_ms": {name: statistics.median(v) for name, v in ms.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +327,10 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=8192, help="jobs per pass timed on the host CPU (cpu_baseline)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum host-CPU time of the cpu_baseline sample")
     ap.add_argument("--no-block-import", action="store_true", help="skip the config-3 latency measurement")
+    ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of corrupted sets (config 4: 1%%)")
+    ap.add_argument("--calls-per-batch", type=int, default=0,
+                    help="calls merged per device super-batch (default: the largest divisor of --steps "
+                         "with <= 163840 sets)")
     args = ap.parse_args()
     rank, world, local = dist_env()
     barrier = Barrier(world)
@@ -246,7 +340,7 @@ def main():
     # device-resident pubkey cache of nkeys interop validators
     t0 = time.perf_counter()
     ctx.keygen(b"".join(interop_sk(i) for i in range(args.nkeys)), cache_first=0, want_pubkeys=False)
-    jobs, expect, key_of = make_gossip_batch(ctx, native, rank, args.nsets, args.nkeys)
+    jobs, expect, key_of = make_gossip_batch(ctx, native, rank, args.nsets, args.nkeys, args.corrupt)
     setup_s = time.perf_counter() - t0
     packed = native.PackedCall(jobs)
 
@@ -259,7 +353,6 @@ def main():
             raise native.DeviceError(native.strerror(rc))
         return list(out), st
 
-    from concurrent.futures import ThreadPoolExecutor
     # unloaded latency: one batch at a time
     lat1 = []
     for _ in range(3):
@@ -267,30 +360,26 @@ def main():
         got, _ = step()
         lat1.append(time.perf_counter() - ts)
         assert got == expect, "verdict mismatch"
-    with ThreadPoolExecutor(max_workers=max(1, args.inflight)) as pool:
-        for got, _ in pool.map(lambda _: step(), range(args.warmup)):
-            assert got == expect, "verdict mismatch in warmup"
+    # Steady state: super-batches of B calls with B | gcd(W, K), so the W-th and the
+    # (W+K)-th completions both fall on super-batch boundaries, and a long coalescing window
+    # so every super-batch fills to B calls (restored after the timed region)
+    ndisp = int(os.environ.get("BGV_DISPATCHERS", "2"))
+    bcalls = args.calls_per_batch or super_batch_calls(args.steps, args.nsets, ndisp)
+    # the window opens on a super-batch boundary: at least `warmup` calls complete before it
+    warm_calls = -(-args.warmup // bcalls) * bcalls
+    ctx.set_batching(bcalls * args.nsets, 200000)
     ctx.profile(1)
-
-    def timed_step(_):
-        ts = time.perf_counter()
-        got, st = step()
-        return time.perf_counter() - ts, got, st
-
     barrier()
     cuda_sync()
-    t_start = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=max(1, args.inflight)) as pool:
-        results = list(pool.map(timed_step, range(args.steps)))
+    win = stream_window(step, expect, warm_calls, args.steps, max(args.inflight, 3 * bcalls))
     cuda_sync()
     barrier()
-    elapsed = time.perf_counter() - t_start
-    lat = [r[0] for r in results]
-    stats = [r[2] for r in results]
-    if any(r[1] != expect for r in results):
-        raise SystemExit("verdict mismatch")
-    elapsed = barrier.max(elapsed)
+    ctx.set_batching(131072, 2000)
+    elapsed = barrier.max(win["elapsed"])
+    lat = win["latencies"]
+    stats = win["stats"]
     kms, launches = ctx.profile(0)
+    roof = roofline_isolated(ctx, native, args.nkeys) if world == 1 or rank == 0 else None
     block = None
     agg = None
     extras = world == 1 and not args.no_block_import  # N=1 only, outside the timed region
@@ -303,33 +392,36 @@ def main():
         total_sets = args.nsets * args.steps * world
         opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["fp_mul_eq"]
         per_set = {"k_prep": opc["k_sig"] + opc["k_hash"] + opc["k_pk[n_pk=1]"], "k_miller": opc["k_miller"]}
-        # HIP-event time per kernel launch (under concurrency a kernel's span includes
-        # its overlap with the other in-flight batches)
+        # timed region: HIP-event time per launch (a kernel's span includes its overlap with
+        # the other in-flight super-batches' kernels on other streams)
         avg = {k: v / max(1, launches) for k, v in kms.items()}
-        dom = max(per_set, key=lambda k: avg.get(k, 0))
-        # sets per verify call, and per launch of the per-set kernels (calls are merged
-        # into device super-batches, so one launch covers several calls)
         slots = statistics.mean(s.sets_verified for s in stats)
-        slots_per_launch = sum(s.sets_verified for s in stats) / max(1, launches)
-        achieved = per_set[dom] * MACS_PER_FP_MUL * slots_per_launch / (avg[dom] * 1e-3)
-        # whole-pipeline VALU figure: every verify kernel's counted work over the step time
-        # closing: one final exponentiation per device group, and (at least) one Fp12
-        # product per slot for the group products
-        per_group = opc["k_final[per group]"] + opc["k_final[group sig pair]"]
         groups = statistics.mean(s.device_groups for s in stats)
+        # whole-pipeline VALU figure: every verify kernel's counted work over the step time
+        per_group = opc["k_final[per group]"] + opc["k_final[group sig pair]"]
         per_slot_close = opc["k_final[per product step]"] + opc["k_final[per slot sig add]"]
         pipeline_macs = ((sum(per_set.values()) + per_slot_close) * slots + per_group * groups) \
             * MACS_PER_FP_MUL * args.steps * world
         pipeline_frac = pipeline_macs / elapsed / (PEAK_MAC_PER_S * world)
-        # HBM bytes per launch of the dominant kernel from the committed PMC passes
-        # (profiles/traffic.json, per slot) scaled to this run's slots per launch
+        # dominant kernel at full occupancy, alone on the device (roofline_isolated): its
+        # algorithmic MACs (set pairs + the group pairs on the same launch) / its HIP-event time
+        rk = roof["kernel_ms"]
+        dom = max(per_set, key=lambda k: rk.get(k, 0))
+        ngr = roof["sets"] // 64
+        work = {"k_miller": roof["sets"] * opc["k_miller"] + ngr * opc["k_final[group sig pair]"],
+                "k_prep": roof["sets"] * per_set["k_prep"]}[dom]
+        achieved = work * MACS_PER_FP_MUL / (rk[dom] * 1e-3)
+        # HBM bytes of that same launch from the committed PMC passes (profiles/r02/traffic.json:
+        # (FETCH_SIZE x 2 + WRITE_SIZE) x 1024, rocprofv3 reports KB) and the algorithmic bytes
         traffic = hbm_gbs = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        tf = os.path.join(ROOT, "profiles", "r02", "traffic.json")
         if os.path.exists(tf):
-            per_slot = json.load(open(tf)).get(dom, {}).get("bytes_per_slot")
-            if per_slot:
-                traffic = per_slot * slots_per_launch
-                hbm_gbs = traffic / (avg[dom] * 1e-3) / 1e9
+            rec = json.load(open(tf)).get(dom, {})
+            if rec.get("sets") == roof["sets"]:
+                traffic = rec["bytes_per_launch"]
+                hbm_gbs = traffic / (rk[dom] * 1e-3) / 1e9
+        alg_bytes = {"k_miller": roof["sets"] * (112 + 336 + 672 + 8 + 160) + ngr * (336 + 672),
+                     "k_prep": roof["sets"] * (160 + 4 + 112 * 1 + 336 * 2 + 112 + 8)}[dom]
         line = {
             "metric": "verified signature sets/sec (node) at 8192-set batches",
             "value": total_sets / elapsed,
@@ -348,8 +440,14 @@ def main():
                     "device-signed; 1%% corrupted (wrong msg / wrong key / bad encoding)" % args.nkeys,
             "config": {"workload": "config4: 8192-set gossip batch (8192 batchable one-set jobs, BGV_MODE_WORKER, "
                                    "batch-fail -> per-job retry)", "sets_per_batch": args.nsets,
-                       "batches_in_flight": args.inflight,
+                       "batches_in_flight": max(args.inflight, 3 * bcalls), "calls_per_super_batch": bcalls,
                        "parallelism": "dp%d (independent batches per GPU)" % world},
+            "timing": "steady state: calls stream with the given number in flight; the window runs from the "
+                      "%d-th to the %d-th completed call (exactly %d calls inside; the %d warmup steps are the "
+                      "first %d completions, rounded up to whole super-batches), super-batches of %d calls so both "
+                      "edges fall on batch boundaries; %d calls completed in all"
+                      % (warm_calls, warm_calls + args.steps, args.steps, args.warmup, warm_calls, bcalls,
+                         win["calls_total"]),
             "kernel_ms_per_launch": avg,
             "retries_per_step": statistics.mean(s.batch_retries for s in stats),
             "call_device_ms": statistics.mean(s.device_ms for s in stats),
@@ -357,9 +455,14 @@ def main():
             "device_groups_per_step": statistics.mean(s.device_groups for s in stats),
             "roofline": {"bound": "valu", "kernel": dom, "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
                          "unit": "TMAC/s (u32 mad)", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
+                         "measured": "one %d-set verify call alone on the device after the timed region (k_miller: "
+                                     "%d set pairs + %d group pairs = one wave per SIMD), HIP events on the "
+                                     "launching stream, median of 2" % (roof["sets"], roof["sets"], ngr),
                          "work_per_set": "%d Fp-mul-eq x %d MAC" % (per_set[dom], MACS_PER_FP_MUL),
-                         "sets_per_launch": slots_per_launch, "ms_per_launch": avg[dom],
-                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "sets_per_launch": roof["sets"], "ms_per_launch": rk[dom],
+                         "kernel_ms_isolated": rk,
+                         "traffic_unit": "HBM bytes per launch (PMC (FETCH_SIZE x 2 + WRITE_SIZE) x 1024)",
+                         "algorithmic_bytes": alg_bytes,
                          "hbm_GBps": hbm_gbs, "hbm_frac_of_8TBps": hbm_gbs / 8000 if hbm_gbs else None,
                          "pipeline_frac": pipeline_frac},
             "setup_s": setup_s,

@@ -143,6 +143,23 @@ int bgv_aggregate_pubkeys(bgv_ctx* ctx, const uint32_t* indices, size_t n, uint8
  * (x.c1 | x.c0 | y.c1 | y.c0). */
 int bgv_hash_to_g2(bgv_ctx* ctx, const uint8_t* msgs, const uint32_t* lens, size_t n, uint8_t* out192);
 
+/* Multi-GPU: one job's batch equation split over processes -------
+ * The reference spreads a call's jobs over worker threads (multithread/index.ts:153-166);
+ * here ONE job (e.g. a whole block range, or config 4 mode (ii)) can span GPUs.  Each rank
+ * passes its shard of the job's sets to bgv_verify_partial, which returns the shard's
+ * randomized Miller-loop product
+ *     prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i)       (before the final exponentiation)
+ * as 576 canonical big-endian bytes (the 12 Fp coefficients in tower order), and
+ *     out_codes[0] = first signature error in set order (-BLST code) or 0,
+ *     out_codes[1] = first pubkey condition: -BLST code, 1 for an infinity aggregate, or 0.
+ * The partials are gathered (RCCL over xGMI, or gloo) and bgv_final_verify multiplies them
+ * and runs ONE final exponentiation: *out_verdict = 1 iff the product is 1 in GT.
+ * The job's outcome is then: the first nonzero signature code in rank order, else the
+ * first pubkey code (1 = infinity aggregate: BLST_PK_IS_INFINITY for >= 2 sets, false for
+ * one), else the verdict (lodestar_amd/shard.py). */
+int bgv_verify_partial(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, uint8_t out576[576], int32_t out_codes[2]);
+int bgv_final_verify(bgv_ctx* ctx, const uint8_t* partials, size_t n, int32_t* out_verdict);
+
 /* SURVEY 8(f) rows beside the verify path -------------------------------- */
 
 /* Deposit-time pubkey validation: bls.PublicKey.fromBytes(pubkey, CoordType.affine,
@@ -175,6 +192,14 @@ int bgv_deposits_verify(bgv_ctx* ctx, const uint8_t* keys48, const uint8_t* msgs
  * bgv_sign writes n x 96-byte compressed signatures sk_i * H(msg_i) (msgs: n x 32 B). */
 int bgv_keygen(bgv_ctx* ctx, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48);
 int bgv_sign(bgv_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, size_t n, uint8_t* out96);
+
+/* Super-batch geometry: verify calls queued within coalesce_us of each other are merged
+ * into one device launch of at most max_batch_slots sets (the GPU form of the pool's
+ * MAX_BUFFERED_SIGS / MAX_BUFFER_WAIT_MS and prepareWork packaging,
+ * multithread/index.ts:39-57,386-401).  max_batch_slots = 0 and coalesce_us = UINT32_MAX
+ * leave a value unchanged.  Defaults: 131072 sets, 2000 us (env BGV_MAX_BATCH_SLOTS,
+ * BGV_COALESCE_US). */
+int bgv_set_batching(bgv_ctx* ctx, uint32_t max_batch_slots, uint32_t coalesce_us);
 
 /* Deterministic batch randomizers for tests (seed != 0: splitmix64 stream;
  * seed == 0: getrandom(), the default). */

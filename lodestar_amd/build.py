@@ -12,7 +12,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libblsgpu.so")
-SOURCES = [os.path.join(CSRC, "bgv_kernels.hip"), os.path.join(CSRC, "bgv_api.cpp")]
+# kernel translation units (compiled in parallel; each carries its own copy of the
+# out-of-line arithmetic with its own register budget) and the host orchestration
+KERNEL_UNITS = ["bgv_k_prep.hip", "bgv_k_miller.hip", "bgv_k_final.hip", "bgv_k_util.hip"]
+SOURCES = [os.path.join(CSRC, f) for f in KERNEL_UNITS] + [os.path.join(CSRC, "bgv_api.cpp")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("BGV_OFFLOAD_ARCH", "gfx950")
 
@@ -43,7 +46,7 @@ def build(force=False, verbose=True, lib=LIB, defines=()):
         return lib
     os.makedirs(OBJ_DIR, exist_ok=True)
     hdr_mtime = max(os.path.getmtime(h) for h in _headers())
-    objs = []
+    objs, procs = [], []
     tag = os.path.basename(lib) + ("." + "_".join(defines) if defines else "")
     for src in SOURCES:
         obj = os.path.join(OBJ_DIR, tag + "." + os.path.basename(src) + ".o")
@@ -54,9 +57,12 @@ def build(force=False, verbose=True, lib=LIB, defines=()):
                    "-c", src, "-o", obj + ".tmp"] + ["-D" + d for d in defines]
             if verbose:
                 print(" ".join(cmd), flush=True)
-            subprocess.check_call(cmd)
-            os.replace(obj + ".tmp", obj)
+            procs.append((subprocess.Popen(cmd), obj))
         objs.append(obj)
+    for p, obj in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, "hipcc " + obj)
+        os.replace(obj + ".tmp", obj)
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -138,6 +138,10 @@ struct Exec {
   Pinned<uint32_t> h_idx;
   Pinned<uint8_t> h_pkb;
   Pinned<int32_t> h_ss, h_ps, h_verdict;
+  void* d_pscratch = nullptr;  // Fp12 products of bgv_verify_partial calls
+  size_t pscratch_cap = 0;
+  uint8_t* d_pout = nullptr;
+  size_t pout_cap = 0;
 };
 
 struct Device {
@@ -248,6 +252,11 @@ struct Call {
   std::vector<std::vector<size_t>> units;  // pending retry units
   std::vector<Part> parts;
   bgv_stats st{};
+  // bgv_verify_partial: the call's Miller-loop product (576 B) and its two status codes
+  uint8_t* partial_out = nullptr;
+  int32_t* partial_codes = nullptr;
+  bgv_job pjob{};
+  int32_t pcode = 0;
   uint32_t slot_base = 0;  // offset of this call's slots in the merged batch
   int rc = BGV_OK;
   // completion
@@ -272,6 +281,9 @@ struct bgv_ctx {
   // BGV_FAULT_INJECT=1 at bgv_init: every super-batch fails as a HIP error would (tests of
   // the device-error path: every job in flight rejects with BGV_E_DEVICE, none resolves false)
   bool fault_inject = false;
+  // super-batch geometry (bgv_set_batching; env defaults at bgv_init)
+  std::atomic<uint32_t> max_slots{BGV_MAX_BATCH_SLOTS};
+  std::atomic<uint32_t> coalesce{BGV_COALESCE_US};
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
   // dispatch
@@ -370,7 +382,7 @@ static int exec_create(Exec* x) {
 
 static void exec_destroy(Exec* x) {
   if (x->main) (void)hipStreamSynchronize(x->main);
-  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb};
+  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb, x->d_pscratch, x->d_pout};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   x->h_slots.release();
@@ -552,6 +564,21 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
       call->st.sets_verified++;
     }
   call->st.device_groups += ngroups;
+  if (call->partial_out) {
+    // first signature error and first pubkey condition in set order (the caller combines
+    // the shards' codes in rank order, as job_precheck does within one job)
+    int32_t sig = 0, pk = 0;
+    for (size_t i = 0; i < call->nsets; ++i) {
+      const int32_t a = call->set_sig[i], q = call->set_pk[i];
+      if (!sig && a != BGV_OK && a != BGV_ST_INFINITY) sig = -a;
+      if (!pk && q == BGV_ST_INFINITY) pk = 1;
+      if (!pk && q != BGV_OK && q != BGV_ST_INFINITY) pk = -q;
+    }
+    call->partial_codes[0] = sig;
+    call->partial_codes[1] = pk;
+    for (size_t j : call->todo) call->code[j] = 1;
+    return;
+  }
   std::vector<char> group_retried(ngroups, 0);
   std::vector<int> unit_of_group(ngroups, -1);
   std::vector<char> seen(call->njobs, 0);
@@ -743,6 +770,32 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       gb += (uint32_t)call->L.groups.size();
     }
   }
+  {
+    // bgv_verify_partial calls: the product of the call's groups (before any retry round
+    // reuses the per-group arrays), serialized on the device
+    uint32_t gb = 0, np = 0, maxg = 0;
+    for (Call* call : calls) {
+      if (call->partial_out) {
+        ++np;
+        maxg = std::max<uint32_t>(maxg, (uint32_t)call->L.groups.size());
+      }
+    }
+    if (np) {
+      if ((rc = grow(reinterpret_cast<uint8_t**>(&x.d_pscratch), &x.pscratch_cap,
+                     bgv_fp12_bytes() * (maxg / 32 + 4))) ||
+          (rc = grow(&x.d_pout, &x.pout_cap, 576)))
+        return rc;
+      for (Call* call : calls) {
+        const uint32_t ng = (uint32_t)call->L.groups.size();
+        if (call->partial_out) {
+          HIPCHK(bgv_launch_partial(b, gb, ng, x.d_pscratch, x.d_pout, x.close));
+          HIPCHK(hipMemcpyAsync(call->partial_out, x.d_pout, 576, hipMemcpyDeviceToHost, x.close));
+          HIPCHK(hipStreamSynchronize(x.close));
+        }
+        gb += ng;
+      }
+    }
+  }
   t_post = ms_since(tp);
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
@@ -805,8 +858,9 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
         for (Call* q : c->queue) n += q->L.slots.size();
         return n;
       };
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(coalesce_us());
-      while (!c->stop && queued_slots() < max_batch_slots() &&
+      const size_t cap = c->max_slots.load();
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(c->coalesce.load());
+      while (!c->stop && queued_slots() < cap &&
              c->qcv.wait_until(lk, until) != std::cv_status::timeout) {
       }
       if (c->queue.empty()) continue;
@@ -814,7 +868,7 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
       while (!c->queue.empty()) {
         Call* call = c->queue.front();
         const size_t n = call->L.slots.size();
-        if (!calls.empty() && slots + n > max_batch_slots()) break;
+        if (!calls.empty() && slots + n > cap) break;
         calls.push_back(call);
         slots += n;
         c->queue.pop_front();
@@ -863,6 +917,8 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     const char* fi = getenv("BGV_FAULT_INJECT");
     c->fault_inject = fi && atoi(fi) > 0;
   }
+  c->max_slots = (uint32_t)max_batch_slots();
+  c->coalesce = (uint32_t)coalesce_us();
   const int n = (devices && ndev > 0) ? ndev : 1;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
@@ -907,6 +963,13 @@ int bgv_destroy(bgv_ctx* c) {
   if (!c) return -BGV_E_ARG;
   bgv_close(c);
   delete c;
+  return BGV_OK;
+}
+
+int bgv_set_batching(bgv_ctx* c, uint32_t max_batch_slots, uint32_t coalesce_us) {
+  if (!c) return -BGV_E_ARG;
+  if (max_batch_slots) c->max_slots = std::max<uint32_t>(max_batch_slots, BGV_WAVE);
+  if (coalesce_us != UINT32_MAX) c->coalesce = coalesce_us;
   return BGV_OK;
 }
 
@@ -1003,6 +1066,70 @@ int bgv_verify_async(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_se
   int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, done, user);
   if (rc != BGV_OK) delete call;
   return rc;
+}
+
+static void fp12_one_bytes(uint8_t out[576]) {
+  memset(out, 0, 576);
+  out[47] = 1;  // c0.c0.c0 = 1, big-endian
+}
+
+int bgv_verify_partial(bgv_ctx* c, const bgv_set* sets, size_t nsets, uint8_t out576[576], int32_t out_codes[2]) {
+  if (!c || !out576 || !out_codes || (nsets && !sets)) return -BGV_E_ARG;
+  out_codes[0] = out_codes[1] = 0;
+  fp12_one_bytes(out576);
+  if (nsets == 0) return c->closed ? -BGV_E_CLOSED : BGV_OK;  // an empty shard: the identity
+  Call* call = new Call();
+  call->partial_out = out576;
+  call->partial_codes = out_codes;
+  call->pjob = bgv_job{0, (uint32_t)nsets, 0};
+  int rc = call_submit(c, call, &call->pjob, 1, sets, nsets, BGV_MODE_PER_JOB, &call->pcode, nullptr, nullptr,
+                       nullptr);
+  if (rc == BGV_OK) {
+    std::unique_lock<std::mutex> lk(call->mu);
+    call->cv.wait(lk, [call] { return call->finished; });
+    rc = call->rc;
+    if (rc == BGV_OK && call->pcode < 0 && call->pcode != -BGV_E_DEVICE) out_codes[0] = call->pcode;  // host-side
+  }
+  delete call;
+  return rc;
+}
+
+int bgv_final_verify(bgv_ctx* c, const uint8_t* partials, size_t n, int32_t* out_verdict) {
+  if (!c || !out_verdict || (n && !partials) || n > (1u << 20)) return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
+  std::lock_guard<std::mutex> lk(c->util_mu);
+  Device& d = c->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  const size_t m = std::max<size_t>(n, 1);
+  std::vector<uint8_t> in(576 * m);
+  if (n) memcpy(in.data(), partials, 576 * n);
+  else fp12_one_bytes(in.data());
+  uint8_t* din = nullptr;
+  void *vals = nullptr, *one = nullptr;
+  bgv_dgroup* dg = nullptr;
+  int32_t *dst = nullptr, *dv = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&din), 576 * m));
+  HIPCHK(hipMalloc(&vals, bgv_fp12_bytes() * m));
+  HIPCHK(hipMalloc(&one, bgv_fp12_bytes()));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dg), sizeof(bgv_dgroup)));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dst), 4 * m));
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dv), 4));
+  const bgv_dgroup g{0, (uint32_t)m};
+  HIPCHK(hipMemcpyAsync(din, in.data(), 576 * m, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(hipMemcpyAsync(dg, &g, sizeof(g), hipMemcpyHostToDevice, d.stream));
+  HIPCHK(bgv_launch_final_verify(din, (uint32_t)m, vals, one, dg, dst, dv, d.stream));
+  std::vector<int32_t> st(m);
+  int32_t v = 0;
+  HIPCHK(hipMemcpyAsync(st.data(), dst, 4 * m, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(&v, dv, 4, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  void* bufs[] = {din, vals, one, dg, dst, dv};
+  for (void* q : bufs) (void)hipFree(q);
+  for (int32_t x : st)
+    if (x) return -BGV_E_ARG;  // a coefficient >= p: not a serialized partial
+  *out_verdict = v;
+  return BGV_OK;
 }
 
 int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out96[96]) {

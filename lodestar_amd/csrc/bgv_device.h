@@ -1,0 +1,66 @@
+// Device-side pieces shared by the kernel translation units (bgv_k_*.hip): the record
+// layouts, the arithmetic headers, launch attributes, wavefront exchange helpers and
+// the slot predicate.  Each kernel unit is compiled on its own (no device linking), so
+// every unit carries its own copy of the out-of-line arithmetic with its own register
+// budget: the per-set units are not constrained by each other's occupancy targets.
+#pragma once
+#include "bgv_layout.h"
+#define BGV_KERNEL_SIDE 1
+#include "bls_hash.h"
+#include "bls_pairing.h"
+#include "bls_team.h"
+
+// Waves per SIMD the verify kernels are register-budgeted for (1: up to 512 VGPRs).
+#ifndef BGV_WPE
+#define BGV_WPE 1
+#endif
+// k_prep runs 3 x nslots lanes of shorter tasks: two waves per SIMD measured faster
+// (36.6 vs 45.3 ms per 131072 slots), the long-chain kernels stay at one.
+#ifndef BGV_WPE_PREP
+#define BGV_WPE_PREP 2
+#endif
+// Sets with at least this many cached pubkeys are aggregated by k_pk_agg's wavefront
+// tree instead of serially on the set's k_prep lane.
+#ifndef BGV_PK_TREE_MIN
+#define BGV_PK_TREE_MIN 16
+#endif
+#define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
+#define BGV_KATTR_PREP __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_PREP, BGV_WPE_PREP)))
+
+// Wavefront exchange of one 32-bit word with lane (l ^ m): ds_swizzle in bit-mask mode
+// within each 32-lane half (m < 32), ds_bpermute across the halves (m = 32).  No LDS
+// storage is allocated: both go through the LDS crossbar only.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (M == 32)
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32u) << 2), (int)v);
+  else
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (M << 10));  // and 0x1f, xor M
+}
+
+template <int M, class P>
+__device__ __forceinline__ P point_xor(const P& p) {
+  constexpr int W = (int)(sizeof(P) / 4);
+  P r;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(&p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+  BGV_UNROLL for (int i = 0; i < W; ++i) o[i] = lane_xor<M>(a[i]);
+  return r;
+}
+
+
+
+// A slot takes part in its group's equation iff it is a set whose signature decoded
+// (valid or infinity) and whose pubkeys aggregated to a finite point; its signature
+// joins the group's sum only when it is not the infinity signature (blst skips those).
+__device__ __forceinline__ bool slot_live(const bgv_dslot& d, int32_t ss, int32_t ps) {
+  return !(d.flags & BGV_SLOT_PAD) && (ss == BGV_ST_OK || ss == BGV_ST_INFINITY) && ps == BGV_ST_OK;
+}
+
+#include "bgv_launch.h"
+
+static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
+
+// Kernel k of a verify launch is bracketed by events kev[2k], kev[2k+1] when profiling.
+#define BGV_MARK(i) \
+  if (s.kev) (void)hipEventRecord(s.kev[i], s.main)

@@ -1,0 +1,195 @@
+// Group closing kernels (gfx950): team-parallel products and the final exponentiation
+// check (bls_team.h), and the Fp12 partial products exchanged across processes
+// (per-GPU Miller-loop products gathered for one final exponentiation).
+#include "bgv_device.h"
+
+// Group closing, team-parallel (bls_team.h): a team of 16 lanes per group, lane c < 12
+// owning one Fp coefficient of the running value; operands exchanged through LDS.
+static __constant__ fp2_t kTeamFrob1[6] = BGV_FROB1;
+static __constant__ fp_t kTeamFrob2[6] = BGV_FROB2;
+
+struct tm_dev_ops {
+  fp_t* A;  // this team's 12 + 12 LDS slots
+  fp_t* B;
+  int c;   // lane within the team, 0..15
+  int cc;  // component computed by this lane (lanes 12..15 duplicate 8..11)
+  __device__ fp_t mul(const fp_t& x, const fp_t& y) {
+    if (c < BGV_TEAM_COMPS) {
+      A[c] = x;
+      B[c] = y;
+    }
+    __syncthreads();
+    const fp_t r = tm_mul_lane(cc, A, B);
+    __syncthreads();
+    return r;
+  }
+  __device__ fp_t sqr(const fp_t& x) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t r = tm_sqr_lane(cc, A);
+    __syncthreads();
+    return r;
+  }
+  __device__ fp_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) { return tm_line_lane(cc, l0, l1, l3); }
+  __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t r = tm_mul_line_lane(cc, A, l0, l1, l3);
+    __syncthreads();
+    return r;
+  }
+  __device__ fp_t conj(const fp_t& x) { return fp_select(((cc >> 1) & 1) != 0, x, fp_neg(x)); }
+  __device__ fp_t frob(const fp_t& x) {
+    if (c < BGV_TEAM_COMPS) A[c] = x;
+    __syncthreads();
+    const fp_t x0 = A[cc & ~1], x1 = A[cc | 1];
+    __syncthreads();
+    return tm_frob_lane(cc, x0, x1, kTeamFrob1[tm_tower_pos(cc)]);
+  }
+  __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(cc)]); }
+  __device__ bool is_fp6(const fp_t& x) {
+    const bool bad = c < BGV_TEAM_COMPS && ((cc >> 1) & 1) && !fp_is_zero(x);
+    const uint64_t m = __ballot(bad);
+    return ((m >> (threadIdx.x & ~(BGV_TEAM - 1))) & 0xffffu) == 0;
+  }
+};
+
+
+#define BGV_FINAL_TEAMS (64 / BGV_TEAM)
+
+extern "C" {
+
+// One team per device group (first pass: the groups of the layout; retry rounds: parts of
+// failed groups), each a contiguous range of <= 64 slots: v = prod f_i * g_g with
+// coefficient-parallel team products (operands straight from the per-slot array), then
+// the final-exponentiation check v^((p^12-1)/r) == 1.  The teams of a wave loop to the
+// wave's longest group, the shorter ones multiplying by 1, so every lane reaches every
+// barrier.
+__global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                  const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
+                                  int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod) {
+  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  __shared__ uint32_t lens[BGV_FINAL_TEAMS];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
+  const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
+  // teams past the end duplicate the last group
+  const uint32_t gg = gi < ngroups ? gi : ngroups - 1;
+  const bgv_dgroup g = groups[gg];
+  if (c == 0) lens[team] = g.n_slots;
+  __syncthreads();
+  uint32_t nmax = 0;
+  BGV_UNROLL for (int t = 0; t < BGV_FINAL_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
+  const int fi = tm_fp_index(cc);
+  const fp_t one_c = cc == 0 ? fp_one() : fp_zero();  // component cc of 1
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
+  constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
+  // the group's signature pair first, then its slots
+  fp_t x = reinterpret_cast<const fp_t*>(gpair + gg)[fi];
+  fp_t y = g.n_slots ? fs[fi] : one_c;
+  BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
+    const fp_t yn = k + 1 < g.n_slots ? fs[kFp12 * (k + 1) + fi] : one_c;  // next operand in flight
+    x = o.mul(x, y);
+    y = yn;
+  }
+  // the group's Miller-loop product, kept for cross-process partials (bgv_verify_partial)
+  if (gprod && gi < ngroups && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
+  const bool one = tm_final_exp_is_one(o, x);
+  if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
+}
+
+// Products of runs of Fp12 values (cross-process partials): team t of the
+// grid multiplies in[t * chunk, min(n, (t + 1) * chunk)) into out[t] (1 for an empty run).
+// Teams of a wave loop to the wave's longest run, multiplying by 1, so every lane reaches
+// every barrier.
+__global__ void BGV_KATTR k_fp12_prod(const fp12_t* __restrict__ in, uint32_t n, uint32_t chunk,
+                                      fp12_t* __restrict__ out, uint32_t nout) {
+  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
+  const uint32_t t = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const uint32_t lo = t * chunk;
+  const uint32_t len = lo < n ? (n - lo < chunk ? n - lo : chunk) : 0;
+  const int fi = tm_fp_index(cc);
+  const fp_t one_c = cc == 0 ? fp_one() : fp_zero();
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  fp_t x = one_c;
+  for (uint32_t k = 0; k < chunk; ++k) {  // chunk is uniform: every team runs chunk products
+    const fp_t y = k < len ? reinterpret_cast<const fp_t*>(in + lo + k)[fi] : one_c;
+    x = o.mul(x, y);
+  }
+  if (t < nout && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(out + t)[fi] = x;
+}
+
+// Fp12 <-> 576 canonical big-endian bytes: the 12 Fp coefficients in tower order
+// (c0.c0.c0, c0.c0.c1, c0.c1.c0, ..., c1.c2.c1), 48 bytes each.
+__global__ void k_fp12_to_bytes(const fp12_t* __restrict__ in, uint8_t* __restrict__ out576) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const fp_t* v = reinterpret_cast<const fp_t*>(in);
+  for (int i = 0; i < 12; ++i) {
+    uint8_t b[48];
+    fp_to_be48(b, fp_from_mont(v[i]));
+    for (int q = 0; q < 48; ++q) out576[48 * i + q] = b[q];
+  }
+}
+
+// n serialized values -> Montgomery Fp12; status[i] = 0, or BGV_BAD_ENCODING for a
+// coefficient >= p.  one[0] receives 1 (the group pair slot of a k_final over the values).
+__global__ void k_fp12_from_bytes(const uint8_t* __restrict__ in, uint32_t n, fp12_t* __restrict__ out,
+                                  int32_t* __restrict__ status, fp12_t* __restrict__ one) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *one = fp12_one();
+  if (i >= n) return;
+  fp_t* v = reinterpret_cast<fp_t*>(out + i);
+  int32_t st = BGV_OK;
+  for (int k = 0; k < 12; ++k) {
+    uint8_t b[48];
+    for (int q = 0; q < 48; ++q) b[q] = in[576ull * i + 48 * k + q];
+    const fp_t r = fp_from_be48(b);
+    if (!fp_raw_lt_p(r)) st = BGV_BAD_ENCODING;
+    v[k] = fp_to_mont(r);
+  }
+  status[i] = st;
+}
+
+}  // extern "C"
+
+// Group closing over b.groups (contiguous slot ranges of <= 64 slots) after
+// bgv_launch_miller (first pass, group pairs already made) or, for a retry round over the
+// same per-slot results, with pairs = true: the parts' signature sums and pairs first.
+hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs) {
+  if (b.ngroups == 0) return hipSuccess;
+  BGV_MARK(4);
+  if (pairs) {
+    const hipError_t e = bgv_launch_gpairs(b, s.main);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                     b.f, b.gpair, b.verdict, b.gprod);
+  BGV_MARK(5);
+  return hipGetLastError();
+}
+// Product of groups [g0, g0 + ng) of the last k_final (b.gprod) -> 576 canonical bytes.
+// scratch: (ng / 32 + 2) Fp12 values.
+hipError_t bgv_launch_partial(const bgv_dev_batch& b, uint32_t g0, uint32_t ng, void* scratch, uint8_t* out576,
+                              hipStream_t st) {
+  fp12_t* tmp = reinterpret_cast<fp12_t*>(scratch);
+  const uint32_t chunk = 32, n1 = (ng + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_fp12_prod, dim3(nblk(n1 ? n1 : 1, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.gprod + g0, ng, chunk,
+                     tmp + 1, n1);
+  hipLaunchKernelGGL(k_fp12_prod, dim3(1), dim3(64), 0, st, tmp + 1, n1, n1 ? n1 : 1, tmp, 1u);
+  hipLaunchKernelGGL(k_fp12_to_bytes, dim3(1), dim3(64), 0, st, tmp, out576);
+  return hipGetLastError();
+}
+size_t bgv_fp12_bytes() { return sizeof(fp12_t); }
+
+// prod of n serialized partials, then the final-exponentiation check (one k_final group)
+hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, void* one, const bgv_dgroup* group,
+                                   int32_t* status, int32_t* verdict, hipStream_t st) {
+  hipLaunchKernelGGL(k_fp12_from_bytes, dim3(nblk(n, 64)), dim3(64), 0, st, in, n, reinterpret_cast<fp12_t*>(vals),
+                     status, reinterpret_cast<fp12_t*>(one));
+  hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, group, 1u, reinterpret_cast<const fp12_t*>(vals),
+                     reinterpret_cast<const fp12_t*>(one), verdict, static_cast<fp12_t*>(nullptr));
+  return hipGetLastError();
+}

@@ -1,0 +1,94 @@
+// Pairing kernels of a verify call (gfx950): the groups' signature sums and the Miller
+// loops of the randomized batch equation of blst's verifyMultipleAggregateSignatures
+// (packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25):
+//   prod_i e(r_i pk_i, H(m_i)) * e(-G1, sum_i r_i sig_i) == 1
+//
+//   k_gsum     per device group (a team of 16 lanes): S_g = sum of the group's r_i sig_i
+//   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)), one pair per lane, and on extra lanes
+//              one per group g_g = MillerLoop(-G1, S_g)
+//   k_gpair    retry rounds: the parts' signature pairs alone
+#include "bgv_device.h"
+
+#define BGV_FINAL_TEAMS (64 / BGV_TEAM)
+
+extern "C" {
+
+// Lanes [0, nslots): f_i = MillerLoop(r pk, H(m)), 1 for slots that do not take part.
+// Lanes [nslots, nslots + ngroups): the group's signature pair MillerLoop(-G1, S_g) (1 for
+// an infinite S_g), so the group pairs run beside the set pairs instead of after them.
+__device__ __forceinline__ fp12_t group_pair(const g2_jac& S) {
+  return jac_is_inf(S) ? fp12_one() : miller_loop1(g1_neg_generator(), S);
+}
+
+__global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                   const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                   const int32_t* __restrict__ sig_status, const int32_t* __restrict__ pk_status,
+                                   fp12_t* __restrict__ f, uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                   fp12_t* __restrict__ gpair) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < nslots) {
+    fp12_t r = fp12_one();
+    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1(rpk[s], h[s]);
+    f[s] = r;
+  } else if (s - nslots < ngroups) {
+    gpair[s - nslots] = group_pair(gsum[s - nslots]);
+  }
+}
+
+// retry rounds: the signature pairs of the round's parts alone
+__global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < ngroups) gpair[g] = group_pair(gsum[g]);
+}
+
+// S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an
+// infinity signature in the accumulator).  A team of 16 lanes per group: lane c sums
+// every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
+__global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                             const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
+                                             const int32_t* __restrict__ sig_status,
+                                             const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum) {
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  g2_jac acc = jac_infinity<fp2_t>();
+  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+    const uint32_t s = g.first_slot + k;
+    const int32_t ss = sig_status[s];
+    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+  }
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (gi < ngroups && c == 0) gsum[gi] = acc;
+}
+
+}  // extern "C"
+
+hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
+  const uint32_t n = b.nslots;
+  if (n == 0) return hipSuccess;
+  // the groups' signature sums, then set pairs and group pairs in one launch
+  hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                     b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
+  BGV_MARK(2);
+  hipLaunchKernelGGL(k_miller, dim3(nblk(n + b.ngroups, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h,
+                     b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+  BGV_MARK(3);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
+  hipError_t e = bgv_launch_prep(b, s);
+  return e != hipSuccess ? e : bgv_launch_miller(b, s);
+}
+
+// retry rounds over parts of failed groups: the parts' signature sums and pairs
+hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
+  if (b.ngroups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
+                     b.rsig, b.sig_status, b.pk_status, b.gsum);
+  hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);
+  return hipGetLastError();
+}

@@ -1,0 +1,193 @@
+// Per-set preparation kernels (gfx950): k_pk_agg and k_prep (see bgv_api.cpp for the
+// launch order of a verify call and bgv_k_miller.hip / bgv_k_final.hip for the rest).
+//
+//   k_pk_agg   (only when a call holds a set with >= BGV_PK_TREE_MIN cached keys) one
+//              wavefront per such set sums its keys with a ds_swizzle/ds_bpermute tree
+//   k_prep     three independent tasks side by side (blockIdx.y):
+//              sig  decompress + subgroup-check the 96-byte signature, then r_i * sig_i
+//                   (Jacobian G2, summed per group by k_gsum)
+//              hash hash_to_G2(signing root) -> H(m_i), Jacobian
+//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i, affine
+#include "bgv_device.h"
+
+extern "C" {
+
+
+// r_i * sig_i of a set whose signature decodes and lies in G2 (else only a status).
+__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
+                                      int32_t* __restrict__ sig_status) {
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  if (d.flags & BGV_SLOT_PAD) {
+    st = BGV_ST_INFINITY;
+  } else if (d.sig_len != 96) {
+    st = BGV_INVALID_SIZE;
+  } else {
+    uint8_t b[96];
+    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
+    g2_aff a;
+    bool inf;
+    st = g2_decompress(&a, &inf, b);
+    if (st == BGV_OK) {
+      if (inf) {
+        st = BGV_ST_INFINITY;  // skipped in the accumulator, as blst does
+      } else {
+        const g2_jac j = jac_from_aff(a);
+        if (!g2_in_subgroup(j))
+          st = BGV_POINT_NOT_IN_GROUP;
+        else
+          rsig[s] = jac_mul_u64(j, d.scalar);  // never infinity: 0 < r < group order
+      }
+    }
+  }
+  sig_status[s] = st;
+}
+
+__device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
+  const bgv_dslot& d = slots[s];
+  if (d.flags & BGV_SLOT_PAD) return;
+  uint8_t msg[32];
+  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
+  h[s] = hash_to_g2(msg, 32);  // stays Jacobian: k_miller adds it with miller_add_jq
+}
+
+// Sum of one set's pubkeys (PublicKey.aggregate, chain/bls/utils.ts:5-16): the k_pk_agg
+// tree sum when the set went through it, else serial mixed additions of cached keys or of
+// 96-byte records (decoded like blst's PublicKey.fromBytes, bls_curve.h g1_deserialize).
+// *st receives the first record's decode error, if any.
+__device__ __noinline__ static g1_jac pk_sum(const bgv_dslot& d, const uint32_t* __restrict__ pk_idx,
+                                      const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
+                                      const g1_jac* __restrict__ pk_agg, uint32_t s, int32_t* st) {
+  g1_jac acc = jac_infinity<fp_t>();
+  const bool cached = (d.flags & BGV_SLOT_PK_CACHED) != 0;
+  const bool tree = pk_agg != nullptr && cached && d.n_pk >= BGV_PK_TREE_MIN;  // summed by k_pk_agg
+  if (tree) return pk_agg[s];
+  for (uint32_t k = 0; k < d.n_pk; ++k) {
+    g1_aff a;
+    if (cached) {
+      a = cache[pk_idx[d.pk_off + k]];
+    } else {
+      uint8_t b[96];
+      const uint8_t* src = pk_bytes + 96ull * (d.pk_off + k);
+      for (int i = 0; i < 96; ++i) b[i] = src[i];
+      bool inf;
+      const int rc = g1_deserialize(&a, &inf, b);
+      if (rc != BGV_OK) {
+        *st = rc;
+        break;
+      }
+      if (inf) continue;
+    }
+    acc = jac_add_aff(acc, a);
+  }
+  return acc;
+}
+
+__device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
+                                     const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                     const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                     int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  if (d.flags & BGV_SLOT_PAD) {
+    pk_status[s] = BGV_ST_INFINITY;
+    return;
+  }
+  const g1_jac acc = pk_sum(d, pk_idx, cache, pk_bytes, pk_agg, s, &st);
+  if (st == BGV_OK) {
+    g1_aff pa;
+    if (!jac_to_aff(&pa, jac_mul_u64(acc, d.scalar)))
+      st = BGV_ST_INFINITY;  // infinity aggregate: BLST_PK_IS_INFINITY / false (job_precheck)
+    else
+      rpk[s] = pa;
+  }
+  pk_status[s] = st;
+}
+
+// Pubkey aggregation of many-key sets as a wavefront tree (one wave per slot): lane l
+// sums the set's cached keys l, l + 64, ... with mixed additions (coalesced gathers),
+// then six butterfly levels of complete Jacobian additions with the partner lane's
+// partial sum (lane ^ 32, 16, ..., 1) exchanged in registers.  Every lane ends with the
+// total; the sum is the same group element as the serial one.  Waves of slots with fewer
+// than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane reads the same slot).
+__global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                               const uint32_t* __restrict__ pk_idx,
+                                               const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blockIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < BGV_PK_TREE_MIN) return;
+  const uint32_t l = threadIdx.x;
+  g1_jac acc = jac_infinity<fp_t>();
+  for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
+  acc = jac_add(acc, point_xor<32>(acc));
+  acc = jac_add(acc, point_xor<16>(acc));
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (l == 0) pk_agg[s] = acc;
+}
+
+// The three independent per-set tasks in one launch (blockIdx.y = task), so one
+// batch keeps 3x the wavefronts in flight on a single stream.
+__global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
+                                      int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
+                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  // hash first: the longest task starts earliest
+  if (blockIdx.y == 0)
+    task_hash(s, slots, h);
+  else if (blockIdx.y == 1)
+    task_sig(s, slots, rsig, sig_status);
+  else
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+}
+
+// PublicKey.aggregate(...).toBytes(uncompressed) over cached keys through the verify
+// path's own code: pk_sum of one slot (k_pk_agg's tree sum for >= BGV_PK_TREE_MIN keys,
+// task_pk's serial sum below), then affine and the 96-byte ZCash encoding.
+__global__ void k_pk_sum_out(const bgv_dslot* __restrict__ slot, const uint32_t* __restrict__ idx,
+                             const g1_aff* __restrict__ cache, const g1_jac* __restrict__ pk_agg,
+                             uint8_t* __restrict__ out96) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int32_t st = BGV_OK;
+  const g1_jac acc = pk_sum(slot[0], idx, cache, nullptr, pk_agg, 0, &st);
+  g1_aff a;
+  const bool fin = jac_to_aff(&a, acc);
+  uint8_t b[96];
+  g1_serialize(b, a, !fin);
+  for (int i = 0; i < 96; ++i) out96[i] = b[i];
+}
+
+}  // extern "C"
+
+hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
+  const uint32_t n = b.nslots;
+  if (n == 0) return hipSuccess;
+  BGV_MARK(0);
+  // k_pk_agg only when some set is large enough; otherwise k_prep sums serially (null pk_agg)
+  const bool tree = b.max_npk >= BGV_PK_TREE_MIN;
+  if (tree)
+    hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
+                       reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
+  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
+                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
+                     tree ? b.pk_agg : nullptr);
+  BGV_MARK(1);
+  return hipGetLastError();
+}
+
+// slot: one device bgv_dslot {PK_CACHED, n_pk = n, pk_off = 0}; agg: one g1_jac of scratch
+hipError_t bgv_launch_aggregate(const bgv_dslot* slot, const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache,
+                                void* agg, uint8_t* out96, hipStream_t st) {
+  const g1_aff* c = reinterpret_cast<const g1_aff*>(cache);
+  g1_jac* a = reinterpret_cast<g1_jac*>(agg);
+  const bool tree = n >= BGV_PK_TREE_MIN;
+  if (tree) hipLaunchKernelGGL(k_pk_agg, dim3(1), dim3(64), 0, st, slot, 1u, idx, c, a);
+  hipLaunchKernelGGL(k_pk_sum_out, dim3(1), dim3(64), 0, st, slot, idx, c, tree ? a : nullptr, out96);
+  return hipGetLastError();
+}

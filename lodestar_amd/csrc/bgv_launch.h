@@ -36,6 +36,7 @@ struct bgv_dev_batch {
   int32_t* pk_status;
   jac_t<fp2_t>* gsum;  // per group: sum of its r_i sig_i
   fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
+  fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
   int32_t* verdict;    // per group
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
@@ -54,6 +55,7 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // pr
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
+hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
 size_t bgv_slot_bytes();
 size_t bgv_group_bytes();
 size_t bgv_cache_entry_bytes();
@@ -73,3 +75,8 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
                                     const uint32_t* count, uint32_t naggs, void* pts, int32_t* status,
                                     uint8_t* out96, hipStream_t st);
 size_t bgv_g2_point_bytes();
+size_t bgv_fp12_bytes();
+hipError_t bgv_launch_partial(const bgv_dev_batch& b, uint32_t g0, uint32_t ng, void* scratch, uint8_t* out576,
+                              hipStream_t st);
+hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, void* one, const bgv_dgroup* group,
+                                   int32_t* status, int32_t* verdict, hipStream_t st);

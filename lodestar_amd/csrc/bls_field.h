@@ -29,7 +29,9 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BGV_HD __host__ __device__ __forceinline__
-#define BGV_NOINLINE __host__ __device__ __noinline__
+// static: every kernel unit (bgv_k_*.hip) carries its own copy (no device linking; the
+// host-side copies must not collide at link time either)
+#define BGV_NOINLINE static __host__ __device__ __noinline__
 #else
 #define BGV_HD inline __attribute__((always_inline))
 #define BGV_NOINLINE __attribute__((noinline))

@@ -37,7 +37,8 @@ EXPORTED_SYMBOLS = [
     "bgv_init", "bgv_close", "bgv_destroy", "bgv_pubkeys_put", "bgv_pubkeys_count", "bgv_verify",
     "bgv_verify_async", "bgv_aggregate_pubkeys", "bgv_hash_to_g2", "bgv_keygen", "bgv_sign",
     "bgv_set_rng_seed", "bgv_strerror", "bgv_device_count", "bgv_profile",
-    "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify",
+    "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify", "bgv_set_batching",
+    "bgv_verify_partial", "bgv_final_verify",
 ]
 
 
@@ -99,6 +100,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_keygen": ([P, P, SZ, ctypes.c_int64, P], ctypes.c_int),
             "bgv_sign": ([P, P, P, SZ, P], ctypes.c_int),
             "bgv_set_rng_seed": ([P, U64], ctypes.c_int),
+            "bgv_set_batching": ([P, U32, U32], ctypes.c_int),
+            "bgv_verify_partial": ([P, P, SZ, P, P], ctypes.c_int),
+            "bgv_final_verify": ([P, P, SZ, P], ctypes.c_int),
             "bgv_strerror": ([ctypes.c_int], ctypes.c_char_p),
             "bgv_device_count": ([], ctypes.c_int),
             "bgv_profile": ([P, ctypes.c_int, P, P, ctypes.c_int, P], ctypes.c_int),
@@ -170,6 +174,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_batching(self, max_batch_slots: int = 0, coalesce_us: int = 0xFFFFFFFF):
+        """Super-batch geometry (bgv_set_batching); 0 / 0xFFFFFFFF leave a value unchanged."""
+        _check(self.lib.bgv_set_batching(self._h, max_batch_slots, coalesce_us))
 
     def set_rng_seed(self, seed: int):
         _check(self.lib.bgv_set_rng_seed(self._h, seed))
@@ -248,6 +256,21 @@ class Context:
         return list(out[:n])
 
     # --- verification -------------------------------------------------------
+    def verify_partial(self, sets) -> tuple:
+        """One job's shard (list of SetSpec) -> (576-byte Miller-loop product, sig_code, pk_code)
+        (bgv_verify_partial)."""
+        packed = PackedCall([(list(sets), False)])
+        out = ctypes.create_string_buffer(576)
+        codes = (ctypes.c_int32 * 2)()
+        _check(self.lib.bgv_verify_partial(self._h, packed.sets, packed.nsets, out, codes))
+        return out.raw, codes[0], codes[1]
+
+    def final_verify(self, partials: Sequence[bytes]) -> bool:
+        """Product of serialized partials and one final exponentiation == 1 (bgv_final_verify)."""
+        v = ctypes.c_int32()
+        _check(self.lib.bgv_final_verify(self._h, _buf(b"".join(partials)), len(partials), ctypes.byref(v)))
+        return v.value == 1
+
     def verify_jobs(self, jobs, mode: int = MODE_WORKER, stats: Optional[BgvStats] = None) -> List[int]:
         """jobs: list of (sets, batchable) with sets = list of SetSpec.  Returns the
         per-job codes (1 valid, 0 invalid, -code error)."""

@@ -53,7 +53,16 @@ typedef struct {
   int closed;                    /* close() was called: every entry point rejects */
   uint32_t inflight;             /* async verifies not yet completed */
   napi_threadsafe_function tsfn; /* completions from the dispatcher threads */
+  int tsfn_released;             /* released by close() or finalized by the runtime */
+  int owners;                    /* the ctx external and the tsfn: freed when both are gone */
 } addon_ctx;
+
+static void addon_unref(addon_ctx* a) {
+  if (--a->owners == 0) {
+    bgv_destroy(a->c);
+    free(a);
+  }
+}
 
 static addon_ctx* get_actx(napi_env env, napi_value v) {
   void* p = NULL;
@@ -110,6 +119,7 @@ typedef struct {
 
 static void verify_call_js(napi_env env, napi_value js_cb, void* context, void* data);
 static void addon_finalize(napi_env env, void* data, void* hint);
+static void tsfn_finalized(napi_env env, void* data, void* hint);
 
 static napi_value js_init(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -135,10 +145,11 @@ static napi_value js_init(napi_env env, napi_callback_info info) {
   if (rc) return throw_code(env, rc);
   addon_ctx* a = (addon_ctx*)calloc(1, sizeof(addon_ctx));
   a->c = ctx;
+  a->owners = 2;
   napi_value out, name;
   if (napi_create_string_utf8(env, "blsgpu.verify.done", NAPI_AUTO_LENGTH, &name) != napi_ok ||
-      napi_create_threadsafe_function(env, NULL, NULL, name, 0, 1, NULL, NULL, NULL, verify_call_js, &a->tsfn) !=
-          napi_ok ||
+      napi_create_threadsafe_function(env, NULL, NULL, name, 0, 1, a, tsfn_finalized, NULL, verify_call_js,
+                                      &a->tsfn) != napi_ok ||
       napi_unref_threadsafe_function(env, a->tsfn) != napi_ok ||
       napi_create_external(env, a, addon_finalize, NULL, &out) != napi_ok) {
     bgv_destroy(ctx);
@@ -158,7 +169,11 @@ static napi_value js_close(napi_env env, napi_callback_info info) {
   addon_ctx* a = get_actx(env, argv[0]);
   if (a && !a->closed) {
     a->closed = 1;
-    bgv_close(a->c);
+    bgv_close(a->c);  /* every queued completion has been handed to the tsfn */
+    if (!a->tsfn_released) {
+      a->tsfn_released = 1;
+      napi_release_threadsafe_function(a->tsfn, napi_tsfn_release);  /* delivers them, then finalizes */
+    }
   }
   return NULL;
 }
@@ -442,7 +457,7 @@ static void verify_call_js(napi_env env, napi_value js_cb, void* context, void* 
   if (env) {
     addon_ctx* a = r->actx;
     settle(env, r);
-    if (--a->inflight == 0) napi_unref_threadsafe_function(env, a->tsfn);
+    if (--a->inflight == 0 && !a->tsfn_released) napi_unref_threadsafe_function(env, a->tsfn);
     free_req(env, r);
   }
 }
@@ -454,15 +469,30 @@ static void verify_done(void* user, int rc) {
   napi_call_threadsafe_function(r->actx->tsfn, r, napi_tsfn_nonblocking);
 }
 
+/* the runtime finalized the tsfn (after close() released it, or at environment teardown) */
+static void tsfn_finalized(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  addon_ctx* a = (addon_ctx*)data;
+  a->tsfn_released = 1;
+  addon_unref(a);
+}
+
 /* the ctx external was collected: no verify references it any more */
 static void addon_finalize(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
   addon_ctx* a = (addon_ctx*)data;
   if (!a) return;
-  napi_release_threadsafe_function(a->tsfn, napi_tsfn_abort);
-  bgv_destroy(a->c);  /* bgv_close first when close() was never called */
-  free(a);
+  if (!a->closed) {
+    a->closed = 1;
+    bgv_close(a->c);
+  }
+  if (!a->tsfn_released) {
+    a->tsfn_released = 1;
+    napi_release_threadsafe_function(a->tsfn, napi_tsfn_abort);
+  }
+  addon_unref(a);
 }
 
 static napi_value js_verify(napi_env env, napi_callback_info info) {
@@ -470,7 +500,15 @@ static napi_value js_verify(napi_env env, napi_callback_info info) {
   napi_value argv[3];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   addon_ctx* a = get_actx(env, argv[0]);
-  if (!a || a->closed) return throw_code(env, -BGV_E_CLOSED);
+  if (!a || a->closed) { /* the Promise rejects (QUEUE_ABORTED), as every verify outcome is async */
+    napi_deferred d;
+    napi_value promise, err, msg;
+    CHECK(env, napi_create_promise(env, &d, &promise));
+    napi_create_string_utf8(env, bgv_strerror(-BGV_E_CLOSED), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, d, err);
+    return promise;
+  }
   verify_req* r = (verify_req*)calloc(1, sizeof(verify_req));
   r->actx = a;
   int32_t mode = 0;

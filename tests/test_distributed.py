@@ -3,8 +3,12 @@
 * shard_bounds: job-boundary partition balanced by set count;
 * ShardedVerify: each rank verifies its shard, verdicts all-gathered — checked on the
   golden verdict vectors, with the C++ CPU restatement standing in for the device as the
-  per-rank verify function (test harness only; on the GPU box the same class wraps
-  native.Context.verify_jobs);
+  per-rank verify function (test harness only; tests/test_gpu_distributed.py runs the same
+  class over native.Context on the GPU);
+* a rank whose device call fails: every rank joins the collective and raises (no hang,
+  no verdict);
+* verify_one_job: the Fp12-partial protocol's code combination in set order (signature
+  errors first, then pubkey conditions, then the verdict) with stand-in partial functions;
 * bench.py's Barrier: barrier + max-over-ranks of the timed region.
 """
 import json
@@ -15,7 +19,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from lodestar_amd.shard import ShardedVerify, shard_bounds
+from lodestar_amd.shard import ShardedVerify, shard_bounds  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -71,6 +75,94 @@ def _worker(rank, world, port, q):
         q.put((rank, got == exp, seen, mx))
     finally:
         dist.destroy_process_group()
+
+
+def _fault_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lodestar_amd import native
+
+        def verify_fn(js):
+            if rank == 1:
+                raise native.DeviceError("BGV_E_DEVICE: HIP device error")
+            return [1] * len(js)
+
+        jobs = [([("s", i)], True) for i in range(6)]
+        try:
+            got = ShardedVerify(verify_fn, dist)(jobs)
+            q.put((rank, "returned %r" % got))
+        except native.DeviceError:
+            q.put((rank, "raised"))
+        # one job: a failing partial on rank 0 raises everywhere too
+        def partial_fn(sets):
+            if rank == 0:
+                raise native.DeviceError("BGV_E_DEVICE: HIP device error")
+            return ONE, 0, 0
+        try:
+            code = ShardedVerify(None, dist, partial_fn=partial_fn, final_fn=lambda p: True).verify_one_job(
+                [("s", i) for i in range(4)])
+            q.put((rank, "one-job returned %r" % code))
+        except native.DeviceError:
+            q.put((rank, "one-job raised"))
+    finally:
+        dist.destroy_process_group()
+
+
+ONE = bytes(47) + b"\x01" + bytes(528)
+BAD = b"\x02" * 576
+
+
+def _one_job_worker(rank, world, port, q):
+    """Stand-in partials: a set is (valid, sig_code, pk_code); the shard's partial is ONE
+    iff every set is valid, and final_fn accepts iff every partial is ONE."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def partial_fn(sets):
+            sc = next((s for _, s, _ in sets if s), 0)
+            pc = next((p for _, _, p in sets if p), 0)
+            return (ONE if all(v for v, _, _ in sets) else BAD), sc, pc
+
+        sv = ShardedVerify(None, dist, partial_fn=partial_fn, final_fn=lambda ps: all(p == ONE for p in ps))
+        ok = [(1, 0, 0)] * 8
+        cases = {
+            "valid": (ok, 1),
+            "invalid_on_rank1": (ok[:6] + [(0, 0, 0)] + ok[7:], 0),
+            # signature errors win over pubkey conditions, the first in set order wins
+            "sig_err_rank1_pk_err_rank0": ([(1, 0, -2)] + ok[1:5] + [(1, -1, 0)] + ok[6:], -1),
+            "two_sig_errs": ([(1, 0, 0), (1, -3, 0)] + ok[2:6] + [(1, -8, 0)] + ok[7:], -3),
+            "pk_infinity": (ok[:5] + [(1, 0, 1)] + ok[6:], -6),
+            "pk_infinity_single_set": ([(1, 0, 1)], 0),
+            "empty": ([], -21),
+        }
+        q.put((rank, {k: sv.verify_one_job(v[0]) == v[1] for k, v in cases.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world=2):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world * (2 if target is _fault_worker else 1)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_device_error_on_one_rank_raises_everywhere():
+    res = _spawn(_fault_worker)
+    assert [r[1] for r in res] == ["one-job raised", "raised", "one-job raised", "raised"], res
+
+
+def test_one_job_code_combination():
+    for rank, ok in _spawn(_one_job_worker):
+        assert all(ok.values()), (rank, ok)
 
 
 def _free_port():
