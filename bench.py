@@ -160,7 +160,7 @@ def block_import_latency(ctx, native, nkeys, runs=100):
             "runs": runs}
 
 
-def aggregate_throughput(ctx, native, nkeys, calls=96, inflight=32):
+def aggregate_throughput(ctx, native, nkeys, calls=384, inflight=128):
     """config 2: 1024 aggregate sets x 128 distinct cached keys (contiguous committees),
     distinct signing roots, all valid, sent as the pool sends them (8 batchable jobs of
     128 sets, index.ts:155-166); `calls` such calls, `inflight` at a time."""
@@ -185,24 +185,54 @@ def aggregate_throughput(ctx, native, nkeys, calls=96, inflight=32):
         return list(out)
 
     assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
+    # enough calls in flight to fill whole super-batches (128 x 1024 sets = 131,072)
+    ctx.set_batching(131072, 20000)
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max_workers=inflight) as pool:
         res = list(pool.map(call, range(calls)))
     dt = time.perf_counter() - t0
+    ctx.set_batching(131072, 2000)
     assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
     return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls, "
                       "%d in flight" % (calls, inflight),
             "value": nsets * calls / dt, "unit": "sets/s", "pubkeys_per_s": nsets * per * calls / dt}
 
 
+def host_cpu():
+    """nproc, model name and clock of the host the CPU leg runs on (/proc/cpuinfo)."""
+    model, mhz = "unknown", None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k = k.strip()
+                if k == "model name" and model == "unknown":
+                    model = v.strip()
+                elif k == "cpu MHz" and mhz is None:
+                    mhz = float(v)
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": affinity, "model": model, "mhz": mhz}
+
+
 def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
-    """The C++ CPU restatement (oracle/cpu, BlsMultiThreadWorkerPool policy: packages of
-    >= 128 sets over `threads` workers, >= 16-job batch chunks, per-job retry) timed on
-    this host on the first `nsample` jobs of the same gossip batch, repeated until at
-    least `min_seconds` of wall time (a bounded sample: the default bench stays within
-    minutes)."""
+    """The C++ CPU restatement (oracle/cpu: blst's batch equation with 64-bit randomizers
+    in width-5 wNAF, 8-pair Miller loops with shared squarings, mulx/adx Montgomery
+    products; BlsMultiThreadWorkerPool policy: packages of >= 128 sets over `threads`
+    workers, >= 16-job batch chunks, per-job retry) timed on this host on the first
+    `nsample` jobs of the same gossip batch, repeated until at least `min_seconds` of wall
+    time (a bounded sample: the default bench stays within minutes).  Workers = the host
+    threads this process may use, capped by BENCH_CPU_THREADS (16 = the GPU box's CPU share
+    per GPU; os.cpu_count() there reports the whole machine).  Also the config-1 row:
+    one 128-set job on ONE core (BlsSingleThreadVerifier, chain/bls/singleThread.ts:7-40,
+    maybeBatch.ts:16-39)."""
     from oracle.cpu import blscpu
-    threads = min(os.cpu_count() or 1, int(os.environ.get("BENCH_CPU_THREADS", "16")))
+    host = host_cpu()
+    threads = min(host["affinity"] or 1, int(os.environ.get("BENCH_CPU_THREADS", "16")))
     keys = sorted(set(key_of[:nsample]))
     pk = blscpu.sk_to_pk96(b"".join(interop_sk(k) for k in keys))
     pk_of = {k: pk[96 * i:96 * i + 96] for i, k in enumerate(keys)}
@@ -217,12 +247,28 @@ def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
         if dt >= min_seconds:
             break
     nverified = nsample * passes
+    # config 1: 128 valid single sets as one non-batchable job, one thread
+    valid = [i for i in range(nsample) if expect[i] == 1][:128]
+    c1 = [([cj[i][0][0] for i in valid], False)]
+    t1 = time.perf_counter()
+    reps = 0
+    while True:
+        assert blscpu.verify_jobs(c1, 1, 1) == [1]
+        reps += 1
+        d1 = time.perf_counter() - t1
+        if d1 >= min(3.0, min_seconds):
+            break
     return {"value": nverified / dt, "unit": "sets/s", "cores": threads, "kind": "port",
-            "sample": "oracle/cpu/blscpu.cpp (C++ restatement, 6x64-bit Montgomery, not blst): %d passes over the "
-                      "first %d jobs of the same 8192-set gossip batch (1%% corrupt, per-job retry), %d worker "
-                      "threads, %.1f s; per-core %.0f sets/s (reference anchor: ~0.9 ms per single verify with "
-                      "blst-native, metrics/lodestar.ts:477)"
-                      % (passes, nsample, threads, dt, nverified / dt / threads)}
+            "host": host,
+            "config1_single_core": {"value": 128 * reps / d1, "unit": "sets/s", "cores": 1,
+                                    "ms_per_job": 1e3 * d1 / reps,
+                                    "sample": "%d x one 128-set job (batch equation), 1 thread" % reps},
+            "sample": "oracle/cpu/blscpu.cpp (C++ restatement with blst's algorithms, not blst itself): %d passes "
+                      "over the first %d jobs of the same 8192-set gossip batch (1%% corrupt, per-job retry), %d "
+                      "worker threads on %s (%s MHz, nproc %s), %.1f s; per-core %.0f sets/s (reference anchor: "
+                      "~0.9 ms per single verify with blst-native, metrics/lodestar.ts:477)"
+                      % (passes, nsample, threads, host["model"], host["mhz"], host["nproc"], dt,
+                         nverified / dt / threads)}
 
 
 def super_batch_calls(steps, nsets, dispatchers=2, max_slots=163840):

@@ -896,6 +896,7 @@ extern "C" {
 
 static void ctx_free_devices(bgv_ctx* c) {
   for (Device& d : c->devs) {
+    if (!d.stream) continue;  // never set up (e.g. an index past the device count)
     (void)hipSetDevice(d.id);
     for (Exec* x : d.execs) exec_destroy(x);
     d.execs.clear();
@@ -934,6 +935,7 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     if (!ok) {
       ctx_free_devices(c);
       delete c;
+      (void)hipGetLastError();  // no stale error for the launch checks of later calls
       return d.id < 0 || d.id >= avail ? -BGV_E_ARG : -BGV_E_DEVICE;
     }
   }

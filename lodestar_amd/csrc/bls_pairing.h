@@ -134,7 +134,9 @@ BGV_HD fp12_t fp12_from_line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) 
 // e(-G1, sum r_i sig_i) is one team loop per device group (bls_team.h).
 BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_aff& p, const g2_jac& q) {
   const fp_t xn = fp_neg(p.x);
+#ifndef BGV_MILLER_JQ_RECOMPUTE
   const miller_jq c = miller_jq_make(q, xn, p.y);
+#endif
   g2_jac t = q;
   fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
@@ -142,6 +144,11 @@ BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_aff& p, const g2_jac& q) {
   fp12_t f = fp12_from_line(l0, l1, l3);
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
+#ifdef BGV_MILLER_JQ_RECOMPUTE
+      // the Jacobian-Q constants for the 5 addition steps only: 112 fewer live VGPRs
+      // across the 63 doubling steps, 5 x 17 Fp products recomputed
+      const miller_jq c = miller_jq_make(q, xn, p.y);
+#endif
       miller_add_jq(t, &l0, &l1, &l3, c);
       f = fp12_mul_line(f, l0, l1, l3);
     }

@@ -17,7 +17,8 @@ LIB = os.path.join(HERE, "libblscpu.so")
 
 def build(force=False):
     src = os.path.join(HERE, "blscpu.cpp")
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, f))
+                                             for f in ("blscpu.cpp", "fp_mulx.h", "Makefile")):
         subprocess.check_call(["make", "-s", "-C", HERE] + (["-B"] if force else []))
     return LIB
 

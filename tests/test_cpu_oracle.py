@@ -43,3 +43,20 @@ def test_verdict_vectors(C, mode):
         jobs.append((sets, jb["batchable"]))
         exp.append(jb["expect"])
     assert C.verify_jobs(jobs, mode, threads=2) == exp
+
+
+@pytest.mark.parametrize("n", [7, 8, 9, 16])
+def test_multi_pair_groups(C, n):
+    """Jobs whose Miller loops span whole and partial 8-pair groups (the sig-sum pair
+    lands in the last group or a group of its own); one wrong set turns the job false
+    and the retry isolates nothing else (worker mode splits the 1-set jobs)."""
+    keys = json.load(open(os.path.join(GOLD, "keys.json")))
+    cases = json.load(open(os.path.join(GOLD, "signatures.json")))["cases"]
+    pk = [bytes.fromhex(k) for k in keys["pk_uncompressed"]]
+    sets = [(pk[c["key"]], bytes.fromhex(c["msg"]), bytes.fromhex(c["sig"])) for c in cases[:n]]
+    bad = list(sets)
+    bad[n // 2] = (sets[n // 2][0], sets[(n // 2) + 1 - n][1], sets[n // 2][2])
+    jobs = [(sets, True), (bad, True)] + [([s], True) for s in bad]
+    exp = [1, 0] + [0 if i == n // 2 else 1 for i in range(n)]
+    assert C.verify_jobs(jobs, 0, threads=2) == exp
+    assert C.verify_jobs(jobs, 1, threads=2) == exp
