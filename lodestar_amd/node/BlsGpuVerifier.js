@@ -21,8 +21,13 @@ const path = require("path");
 const addon = require(path.join(__dirname, "blsgpu.node"));
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:39
-const MAX_BUFFERED_SIGS = 32; // index.ts:48 (the GPU prefers larger; see opts)
-const MAX_BUFFER_WAIT_MS = 100; // index.ts:57
+// Batchable buffering (index.ts:48,57 use 32 sets / 100 ms for CPU workers).  One device call
+// verifies up to ~163k sets in the time of a few hundred, so the GPU wants every set the
+// gossip queues hold (<= 64 concurrent validations each, network/gossip/validation/queue.ts:14)
+// in as few calls as possible: flush at 1024 buffered sets or after 20 ms, and let the
+// library's dispatchers merge the calls that are in flight together (DESIGN.md §3).
+const MAX_BUFFERED_SIGS = 1024;
+const MAX_BUFFER_WAIT_MS = 20;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
 
@@ -79,6 +84,7 @@ class BlsGpuVerifier {
   constructor(opts = {}, modules = {}) {
     this.metrics = modules.metrics || null;
     this.ctx = opts.ctx || addon.init(opts.devices || []);
+    this.pendingPubkeys = [];
     this.blsVerifyAllMultiThread = opts.blsVerifyAllMultiThread || false;
     this.maxBufferedSigs = opts.maxBufferedSigs || MAX_BUFFERED_SIGS;
     this.maxBufferWaitMs = opts.maxBufferWaitMs || MAX_BUFFER_WAIT_MS;
@@ -92,7 +98,38 @@ class BlsGpuVerifier {
     }
   }
 
+  /**
+   * Index2PubkeyCache growth -> device cache (INTEGRATION.md §2): a function for
+   * state-transition's pubkey-added hook, called with (index, 48-byte pubkey, PublicKey).  It
+   * tags the PublicKey with .index (so sets built by the reference's producers travel as
+   * indices) and queues the key; queued keys go to the device in contiguous runs before the
+   * next verification or every 65,536 keys.
+   */
+  pubkeyAddedHook() {
+    return (index, pubkey, pk) => {
+      if (pk && typeof pk === "object") pk.index = index;
+      this.pendingPubkeys.push([index, pubkey]);
+      if (this.pendingPubkeys.length >= 65536) this.flushPubkeys();
+    };
+  }
+
+  flushPubkeys() {
+    const p = this.pendingPubkeys;
+    if (p.length === 0 || this.closed) return;
+    this.pendingPubkeys = [];
+    p.sort((a, b) => a[0] - b[0]);
+    for (let i = 0; i < p.length; ) {
+      let j = i + 1;
+      while (j < p.length && p[j][0] === p[j - 1][0] + 1) j++;
+      const buf = new Uint8Array(48 * (j - i));
+      for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
+      addon.pubkeysPut(this.ctx, p[i][0], buf, 48);
+      i = j;
+    }
+  }
+
   async verifySignatureSets(sets, opts = {}) {
+    this.flushPubkeys();
     const nAgg = getAggregatedPubkeysCount(sets);
     this.counters.aggregatedPubkeys += nAgg;
     if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(nAgg);
