@@ -3,59 +3,8 @@
 // (per-GPU Miller-loop products gathered for one final exponentiation).
 #include "bgv_device.h"
 
-// Group closing, team-parallel (bls_team.h): a team of 16 lanes per group, lane c < 12
-// owning one Fp coefficient of the running value; operands exchanged through LDS.
-static __constant__ fp2_t kTeamFrob1[6] = BGV_FROB1;
-static __constant__ fp_t kTeamFrob2[6] = BGV_FROB2;
+#include "bgv_team_dev.h"
 
-struct tm_dev_ops {
-  fp_t* A;  // this team's 12 + 12 LDS slots
-  fp_t* B;
-  int c;   // lane within the team, 0..15
-  int cc;  // component computed by this lane (lanes 12..15 duplicate 8..11)
-  __device__ fp_t mul(const fp_t& x, const fp_t& y) {
-    if (c < BGV_TEAM_COMPS) {
-      A[c] = x;
-      B[c] = y;
-    }
-    __syncthreads();
-    const fp_t r = tm_mul_lane(cc, A, B);
-    __syncthreads();
-    return r;
-  }
-  __device__ fp_t sqr(const fp_t& x) {
-    if (c < BGV_TEAM_COMPS) A[c] = x;
-    __syncthreads();
-    const fp_t r = tm_sqr_lane(cc, A);
-    __syncthreads();
-    return r;
-  }
-  __device__ fp_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) { return tm_line_lane(cc, l0, l1, l3); }
-  __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
-    if (c < BGV_TEAM_COMPS) A[c] = x;
-    __syncthreads();
-    const fp_t r = tm_mul_line_lane(cc, A, l0, l1, l3);
-    __syncthreads();
-    return r;
-  }
-  __device__ fp_t conj(const fp_t& x) { return fp_select(((cc >> 1) & 1) != 0, x, fp_neg(x)); }
-  __device__ fp_t frob(const fp_t& x) {
-    if (c < BGV_TEAM_COMPS) A[c] = x;
-    __syncthreads();
-    const fp_t x0 = A[cc & ~1], x1 = A[cc | 1];
-    __syncthreads();
-    return tm_frob_lane(cc, x0, x1, kTeamFrob1[tm_tower_pos(cc)]);
-  }
-  __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(cc)]); }
-  __device__ bool is_fp6(const fp_t& x) {
-    const bool bad = c < BGV_TEAM_COMPS && ((cc >> 1) & 1) && !fp_is_zero(x);
-    const uint64_t m = __ballot(bad);
-    return ((m >> (threadIdx.x & ~(BGV_TEAM - 1))) & 0xffffu) == 0;
-  }
-};
-
-
-#define BGV_FINAL_TEAMS (64 / BGV_TEAM)
 
 extern "C" {
 

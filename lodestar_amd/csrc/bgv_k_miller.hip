@@ -7,9 +7,16 @@
 //   k_miller   f_i = MillerLoop(r_i pk_i, H(m_i)), one pair per lane, and on extra lanes
 //              one per group g_g = MillerLoop(-G1, S_g)
 //   k_gpair    retry rounds: the parts' signature pairs alone
+//   k_miller_team  the latency path for small calls: the same pairs, one per team of 16
+//              lanes (bgv_tmiller.h), ~10x lower latency per pair than one lane
 #include "bgv_device.h"
+#include "bgv_team_dev.h"
+#include "bgv_tmiller.h"
 
-#define BGV_FINAL_TEAMS (64 / BGV_TEAM)
+#include <stdlib.h>
+
+static __constant__ uint8_t kTmProg[TMP_TABLE_BYTES] = TMP_TABLE_INIT;
+
 
 extern "C" {
 
@@ -64,7 +71,106 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
   if (gi < ngroups && c == 0) gsum[gi] = acc;
 }
 
+// One Miller loop per team of 16 lanes: pairs [0, nslots) are the sets' e(r pk, H(m)),
+// pairs [nslots, nslots + ngroups) the groups' e(-G1, S_g).  The twist point runs the
+// generated rounds (bgv_tmiller_prog.h) on the team's LDS slots, the Fp12 accumulator is
+// coefficient-parallel.  Teams past the end (and pairs that take no part) compute on
+// zeros and store 1 or nothing, so every lane reaches every barrier.
+__global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                    const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                                    const int32_t* __restrict__ sig_status,
+                                                    const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
+                                                    uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                                    fp12_t* __restrict__ gpair) {
+  __shared__ uint8_t prog[TMP_TABLE_BYTES];
+  __shared__ fp_t S[BGV_FINAL_TEAMS][TMP_NSLOT];
+  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  for (int i = threadIdx.x; i < TMP_TABLE_BYTES; i += 64) prog[i] = kTmProg[i];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
+  const uint32_t total = nslots + ngroups;
+  const uint32_t u = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const uint32_t uu = u < total ? u : total - 1;
+  const bool set_pair = uu < nslots;
+  bool live;
+  const fp_t* qsrc;
+  if (set_pair) {
+    live = slot_live(slots[uu], sig_status[uu], pk_status[uu]);
+    qsrc = reinterpret_cast<const fp_t*>(h + uu);
+  } else {
+    qsrc = reinterpret_cast<const fp_t*>(gsum + (uu - nslots));
+    live = !jac_is_inf(gsum[uu - nslots]);
+  }
+  fp_t* Sm = S[team];
+  if (c < 6) {
+    const fp_t v = live ? qsrc[c] : fp_zero();
+    Sm[TMP_S_QX + c] = v;
+    Sm[TMP_S_BANK0 + c] = v;
+  } else if (c < 8) {
+    const g1_aff P = set_pair ? rpk[uu] : g1_neg_generator();
+    const fp_t v = c == 6 ? fp_neg(P.x) : P.y;
+    Sm[c == 6 ? TMP_S_XN : TMP_S_YP] = live ? v : fp_zero();
+  } else if (c == 8) {
+    Sm[TMP_S_ONE] = fp_one();
+  }
+  __syncthreads();
+  auto run = [&](int off) {
+    int pos = off;
+    const int nr = prog[pos++];
+    for (int r = 0; r < nr; ++r) {
+      const int T = prog[pos], M = prog[pos + 1];
+      pos += 2;
+      const int rb = tmp_rec_bytes(T, M);
+      int out;
+      const fp_t v = tmp_lane(Sm, prog + pos + c * rb, T, M, &out);
+      Sm[out] = v;  // no slot is read and written in one round (tools/gen_tmiller.py)
+      __syncthreads();
+      pos += BGV_TEAM * rb;
+    }
+  };
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  run(TMP_INIT);
+  run(TMP_DBL0);
+  int bank = 1;
+  fp2_t l0 = {Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]}, l1 = {Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]},
+        l3 = {Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+  fp_t x = o.line(l0, l1, l3);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (tmp_add_at(i)) {
+      run(bank ? TMP_ADD1 : TMP_ADD0);
+      bank ^= 1;
+      l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
+      l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
+      l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+      x = o.mul_line(x, l0, l1, l3);
+    }
+    x = o.sqr(x);
+    run(bank ? TMP_DBL1 : TMP_DBL0);
+    bank ^= 1;
+    l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
+    l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
+    l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+    x = o.mul_line(x, l0, l1, l3);
+  }
+  x = o.conj(x);
+  if (u < total && c < BGV_TEAM_COMPS) {
+    fp12_t* dst = set_pair ? f + uu : gpair + (uu - nslots);
+    reinterpret_cast<fp_t*>(dst)[tm_fp_index(cc)] = live ? x : (cc == 0 ? fp_one() : fp_zero());
+  }
+}
+
 }  // extern "C"
+
+// Calls with at most this many pairs (sets + groups) take the team loop: one lane per pair
+// leaves the chip idle and runs ~13 ms however small the call; a team of 16 lanes per pair
+// finishes in a fraction of that.  BGV_TEAM_MILLER_MAX overrides (0 disables).
+static uint32_t team_miller_max() {
+  static const uint32_t v = [] {
+    const char* e = getenv("BGV_TEAM_MILLER_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 4096u;
+  }();
+  return v;
+}
 
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
@@ -73,8 +179,12 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
                      b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
   BGV_MARK(2);
-  hipLaunchKernelGGL(k_miller, dim3(nblk(n + b.ngroups, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h,
-                     b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+  if (n + b.ngroups <= team_miller_max())
+    hipLaunchKernelGGL(k_miller_team, dim3(nblk(n + b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, n,
+                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+  else
+    hipLaunchKernelGGL(k_miller, dim3(nblk(n + b.ngroups, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h,
+                       b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
   BGV_MARK(3);
   return hipGetLastError();
 }
@@ -89,6 +199,10 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum);
-  hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);
+  if (b.ngroups <= team_miller_max())
+    hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u, b.rpk,
+                       b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+  else
+    hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);
   return hipGetLastError();
 }

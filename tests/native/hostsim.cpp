@@ -9,6 +9,7 @@
 #include "../../lodestar_amd/csrc/bls_hash.h"
 #include "../../lodestar_amd/csrc/bls_pairing.h"
 #include "../../lodestar_amd/csrc/bls_team.h"
+#include "../../lodestar_amd/csrc/bgv_tmiller.h"
 
 static fp_t in_fp(const uint8_t* be) { return fp_to_mont(fp_from_be48(be)); }
 static void out_fp(uint8_t* be, const fp_t& a) { fp_to_be48(be, fp_from_mont(a)); }
@@ -221,6 +222,10 @@ void hs_miller_loop1(uint8_t* out, const uint8_t* p, const uint8_t* q) {
 void hs_team_miller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
   tm_emu_ops o;
   out_fp12(out, tm_emu_to_fp12(tm_miller_loop<tm_emu_t>(o, in_g1(p), jac_scaled(in_g2(q)))));
+}
+// the latency path's team loop (bgv_tmiller.h: table-driven twist-point rounds + team Fp12)
+void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
+  out_fp12(out, tm_team_miller_host(in_g1(p), jac_scaled(in_g2(q))));
 }
 void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   tm_emu_ops o;

@@ -268,6 +268,20 @@ def test_miller_loop1_and_team_loop(L):
     assert fe(m1.raw) == fe(ref.raw)
 
 
+def test_table_driven_team_miller_loop(L):
+    """The latency path's team Miller loop (bgv_tmiller.h: generated twist-point rounds,
+    tools/gen_tmiller.py, and the coefficient-parallel Fp12 accumulator), emulated lane by
+    lane, equals miller_loop1 exactly (same formulas, same line scaling) for random pairs
+    and for -G1 with a random Q."""
+    for k in range(3):
+        p = o.g1_mul(o.G1, rnd.randrange(1, o.R)) if k else o.g1_neg(o.G1)
+        q = g2_rand_in_group()
+        m1, tm = hs.buf(576), hs.buf(576)
+        L.hs_miller_loop1(m1, hs.g1_b(p), hs.g2_b(q))
+        L.hs_tmiller(tm, hs.g1_b(p), hs.g2_b(q))
+        assert tm.raw == m1.raw
+
+
 def test_team_mul_line(L):
     """Coefficient-parallel product with a sparse line equals the tower formula."""
     for _ in range(4):
