@@ -4,6 +4,7 @@
 // every unit carries its own copy of the out-of-line arithmetic with its own register
 // budget: the per-set units are not constrained by each other's occupancy targets.
 #pragma once
+#include <stdlib.h>
 #include "bgv_layout.h"
 #define BGV_KERNEL_SIDE 1
 #include "bls_hash.h"
@@ -60,6 +61,18 @@ __device__ __forceinline__ bool slot_live(const bgv_dslot& d, int32_t ss, int32_
 #include "bgv_launch.h"
 
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
+
+// Latency path (small calls): at most this many pairs (sets + groups) take the split
+// k_prep_a / k_prep_b and the team Miller loop instead of one lane per set and task, which
+// wins while the chip would otherwise sit mostly idle (one lane per set runs ~13 ms in
+// k_miller however small the call).  BGV_LATENCY_MAX overrides (0 disables).
+static inline uint32_t bgv_latency_max() {
+  static const uint32_t v = [] {
+    const char* e = getenv("BGV_LATENCY_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 16384u;
+  }();
+  return v;
+}
 
 // Kernel k of a verify launch is bracketed by events kev[2k], kev[2k+1] when profiling.
 #define BGV_MARK(i) \

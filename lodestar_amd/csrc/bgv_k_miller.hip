@@ -13,8 +13,6 @@
 #include "bgv_team_dev.h"
 #include "bgv_tmiller.h"
 
-#include <stdlib.h>
-
 static __constant__ uint8_t kTmProg[TMP_TABLE_BYTES] = TMP_TABLE_INIT;
 
 
@@ -161,17 +159,6 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
 
 }  // extern "C"
 
-// Calls with at most this many pairs (sets + groups) take the team loop: one lane per pair
-// leaves the chip idle and runs ~13 ms however small the call; a team of 16 lanes per pair
-// finishes in a fraction of that.  BGV_TEAM_MILLER_MAX overrides (0 disables).
-static uint32_t team_miller_max() {
-  static const uint32_t v = [] {
-    const char* e = getenv("BGV_TEAM_MILLER_MAX");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 4096u;
-  }();
-  return v;
-}
-
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
@@ -179,7 +166,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
                      b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
   BGV_MARK(2);
-  if (n + b.ngroups <= team_miller_max())
+  if (n + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(n + b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, n,
                        b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
   else
@@ -199,7 +186,7 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum);
-  if (b.ngroups <= team_miller_max())
+  if (b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u, b.rpk,
                        b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
   else

@@ -3,6 +3,11 @@
 //
 //   k_pk_agg   (only when a call holds a set with >= BGV_PK_TREE_MIN cached keys) one
 //              wavefront per such set sums its keys with a ds_swizzle/ds_bpermute tree
+//   k_prep_a / k_prep_b   the latency path for small calls (bgv_latency_max): the same
+//              work over two launches with twice the lanes per set, so the longest chain
+//              per lane roughly halves: (a) one SSWU map + isogeny per lane for u0 and u1,
+//              the signature's decompression, the pubkey task; (b) the cofactor clearing of
+//              q0 + q1, and the signature's subgroup check beside r_i * sig_i
 //   k_prep     three independent tasks side by side (blockIdx.y):
 //              sig  decompress + subgroup-check the 96-byte signature, then r_i * sig_i
 //                   (Jacobian G2, summed per group by k_gsum)
@@ -129,6 +134,90 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   if (l == 0) pk_agg[s] = acc;
 }
 
+// ---- latency path ------------------------------------------------------------------------
+// f[s] (576 B, written by k_miller only later) holds the split's intermediates:
+// q1 = the u1 map's point (g2_jac, 288 B) at offset 0, the decoded signature (g2_aff) at 288.
+__device__ __forceinline__ g2_jac* split_q1(fp12_t* f, uint32_t s) { return reinterpret_cast<g2_jac*>(f + s); }
+__device__ __forceinline__ g2_aff* split_sig(fp12_t* f, uint32_t s) {
+  return reinterpret_cast<g2_aff*>(reinterpret_cast<uint8_t*>(f + s) + sizeof(g2_jac));
+}
+static_assert(sizeof(g2_jac) + sizeof(g2_aff) <= sizeof(fp12_t), "split intermediates fit in f[s]");
+
+// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), isogeny included
+__device__ __noinline__ void task_map(uint32_t s, int which, const bgv_dslot* __restrict__ slots, g2_jac* out) {
+  const bgv_dslot& d = slots[s];
+  if (d.flags & BGV_SLOT_PAD) return;
+  uint8_t msg[32];
+  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
+  fp2_t u0, u1, x, y;
+  hash_to_field_fp2(&u0, &u1, msg, 32);
+  sswu_g2(&x, &y, which ? u1 : u0, fp_sqrt_minus5());
+  *out = iso_map_g2(x, y);
+}
+
+// task_sig's decoding half: status, and the affine point when it decodes to a finite point
+__device__ __noinline__ void task_sig_decode(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* out,
+                                             int32_t* __restrict__ sig_status) {
+  const bgv_dslot& d = slots[s];
+  int32_t st = BGV_ST_OK;
+  if (d.flags & BGV_SLOT_PAD) {
+    st = BGV_ST_INFINITY;
+  } else if (d.sig_len != 96) {
+    st = BGV_INVALID_SIZE;
+  } else {
+    uint8_t b[96];
+    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
+    g2_aff a;
+    bool inf;
+    st = g2_decompress(&a, &inf, b);
+    if (st == BGV_OK) {
+      if (inf)
+        st = BGV_ST_INFINITY;
+      else
+        *out = a;
+    }
+  }
+  sig_status[s] = st;
+}
+
+__global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
+                                        fp12_t* __restrict__ f, int32_t* __restrict__ sig_status,
+                                        const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                        const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                        int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  if (blockIdx.y == 0)
+    task_map(s, 0, slots, h + s);
+  else if (blockIdx.y == 1)
+    task_map(s, 1, slots, split_q1(f, s));
+  else if (blockIdx.y == 2)
+    task_sig_decode(s, slots, split_sig(f, s), sig_status);
+  else
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+}
+
+__global__ void BGV_KATTR_PREP k_prep_b(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
+                                        fp12_t* __restrict__ f, g2_jac* __restrict__ rsig,
+                                        int32_t* __restrict__ sig_status) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const bgv_dslot& d = slots[s];
+  if (d.flags & BGV_SLOT_PAD) return;
+  if (blockIdx.y == 0) {
+    h[s] = g2_clear_cofactor(jac_add(h[s], *split_q1(f, s)));
+    return;
+  }
+  // the decode status is final unless it is OK (then only the subgroup lane may change it)
+  if (sig_status[s] != BGV_ST_OK) return;
+  const g2_jac j = jac_from_aff(*split_sig(f, s));
+  if (blockIdx.y == 1) {
+    if (!g2_in_subgroup(j)) sig_status[s] = BGV_POINT_NOT_IN_GROUP;
+  } else {
+    rsig[s] = jac_mul_u64(j, d.scalar);  // unused unless the subgroup lane leaves the status OK
+  }
+}
+
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
@@ -174,9 +263,17 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   if (tree)
     hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
                        reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
-  hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
-                     b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                     tree ? b.pk_agg : nullptr);
+  if (n + b.ngroups <= bgv_latency_max()) {
+    hipLaunchKernelGGL(k_prep_a, dim3(nblk(n, 64), 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status,
+                       b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
+                       tree ? b.pk_agg : nullptr);
+    hipLaunchKernelGGL(k_prep_b, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig,
+                       b.sig_status);
+  } else {
+    hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
+                       b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
+                       tree ? b.pk_agg : nullptr);
+  }
   BGV_MARK(1);
   return hipGetLastError();
 }
