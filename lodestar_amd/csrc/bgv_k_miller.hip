@@ -22,11 +22,11 @@ extern "C" {
 // Lanes [nslots, nslots + ngroups): the group's signature pair MillerLoop(-G1, S_g) (1 for
 // an infinite S_g), so the group pairs run beside the set pairs instead of after them.
 __device__ __forceinline__ fp12_t group_pair(const g2_jac& S) {
-  return jac_is_inf(S) ? fp12_one() : miller_loop1(g1_neg_generator(), S);
+  return jac_is_inf(S) ? fp12_one() : miller_loop1(jac_from_aff(g1_neg_generator()), S);
 }
 
 __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                   const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                   const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
                                    const int32_t* __restrict__ sig_status, const int32_t* __restrict__ pk_status,
                                    fp12_t* __restrict__ f, uint32_t ngroups, const g2_jac* __restrict__ gsum,
                                    fp12_t* __restrict__ gpair) {
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
 // coefficient-parallel.  Teams past the end (and pairs that take no part) compute on
 // zeros and store 1 or nothing, so every lane reaches every barrier.
 __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                                    const g1_aff* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                                    const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
                                                     const int32_t* __restrict__ sig_status,
                                                     const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
                                                     uint32_t ngroups, const g2_jac* __restrict__ gsum,
@@ -104,11 +104,12 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
     const fp_t v = live ? qsrc[c] : fp_zero();
     Sm[TMP_S_QX + c] = v;
     Sm[TMP_S_BANK0 + c] = v;
-  } else if (c < 8) {
-    const g1_aff P = set_pair ? rpk[uu] : g1_neg_generator();
-    const fp_t v = c == 6 ? fp_neg(P.x) : P.y;
-    Sm[c == 6 ? TMP_S_XN : TMP_S_YP] = live ? v : fp_zero();
-  } else if (c == 8) {
+  } else if (c < 9) {
+    // P in Jacobian form (bls_pairing.h miller_p): -X Z, Y, Z^3
+    const g1_jac P = set_pair ? rpk[uu] : jac_from_aff(g1_neg_generator());
+    const fp_t v = c == 6 ? fp_neg(fp_mul(P.x, P.z)) : (c == 7 ? P.y : fp_mul(fp_sqr(P.z), P.z));
+    Sm[c == 6 ? TMP_S_XN : (c == 7 ? TMP_S_YP : TMP_S_ZP3)] = live ? v : fp_zero();
+  } else if (c == 9) {
     Sm[TMP_S_ONE] = fp_one();
   }
   __syncthreads();

@@ -12,7 +12,7 @@
 //              sig  decompress + subgroup-check the 96-byte signature, then r_i * sig_i
 //                   (Jacobian G2, summed per group by k_gsum)
 //              hash hash_to_G2(signing root) -> H(m_i), Jacobian
-//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i, affine
+//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i (Jacobian)
 #include "bgv_device.h"
 
 extern "C" {
@@ -90,7 +90,7 @@ __device__ __noinline__ static g1_jac pk_sum(const bgv_dslot& d, const uint32_t*
 
 __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                     const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                     const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
@@ -100,11 +100,12 @@ __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ s
   }
   const g1_jac acc = pk_sum(d, pk_idx, cache, pk_bytes, pk_agg, s, &st);
   if (st == BGV_OK) {
-    g1_aff pa;
-    if (!jac_to_aff(&pa, jac_mul_u64(acc, d.scalar)))
+    // Jacobian: the Miller loop takes P projectively (bls_pairing.h miller_p), no inversion
+    const g1_jac rp = jac_mul_u64(acc, d.scalar);
+    if (jac_is_inf(rp))
       st = BGV_ST_INFINITY;  // infinity aggregate: BLST_PK_IS_INFINITY / false (job_precheck)
     else
-      rpk[s] = pa;
+      rpk[s] = rp;
   }
   pk_status[s] = st;
 }
@@ -183,7 +184,7 @@ __device__ __noinline__ void task_sig_decode(uint32_t s, const bgv_dslot* __rest
 __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
                                         fp12_t* __restrict__ f, int32_t* __restrict__ sig_status,
                                         const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                        const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                        const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
                                         int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
@@ -223,7 +224,7 @@ __global__ void BGV_KATTR_PREP k_prep_b(const bgv_dslot* __restrict__ slots, uin
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
                                       int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
                                       const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                      const uint8_t* __restrict__ pk_bytes, g1_aff* __restrict__ rpk,
+                                      const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
                                       int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;

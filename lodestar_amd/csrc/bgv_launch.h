@@ -29,7 +29,7 @@ struct bgv_dev_batch {
   // carved per-slot / per-group scratch
   jac_t<fp2_t>* rsig;  // r_i * sig_i (Jacobian), summed per group by k_final
   jac_t<fp2_t>* h;     // H(m_i), Jacobian
-  aff_t<fp_t>* rpk;    // r_i * aggregated pubkey, affine
+  jac_t<fp_t>* rpk;    // r_i * aggregated pubkey, Jacobian
   fp12_t* f;           // per-slot Miller loop value e(r_i pk_i, H(m_i))
   jac_t<fp_t>* pk_agg;  // wavefront-tree sum of a many-key set's cached pubkeys (k_pk_agg)
   int32_t* sig_status;

@@ -212,15 +212,21 @@ BGV_NOINLINE bool fp2_sqrt_or_z(fp2_t* y, const fp2_t& g, const fp_t& sqrt_m5) {
   return is_sq;
 }
 
-// returns the SWU point on E2' in affine coordinates
-BGV_NOINLINE void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
-  const fp2_t A = BGV_SSWU_A, B = BGV_SSWU_B, Z = BGV_SSWU_Z;
+// SWU on E2' in two halves so that two maps can share one inversion (Montgomery's trick):
+// sswu_den gives den = Z^2 u^4 + Z u^2 (and Z u^2), sswu_finish takes 1/den (any value when
+// den == 0: the exceptional case uses x1 = B / (Z A) and never reads it).
+BGV_HD fp2_t sswu_den(const fp2_t& u, fp2_t* zu2) {
+  const fp2_t Z = BGV_SSWU_Z;
+  *zu2 = fp2_mul(Z, fp2_sqr(u));
+  return fp2_add(fp2_sqr(*zu2), *zu2);
+}
+
+BGV_NOINLINE void sswu_finish(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp2_t& zu2, const fp2_t& den,
+                              const fp2_t& den_inv, const fp_t& sqrt_m5) {
+  const fp2_t A = BGV_SSWU_A, B = BGV_SSWU_B;
   const fp2_t bza = BGV_SSWU_B_OVER_ZA, mba = BGV_SSWU_MINUS_B_OVER_A;
-  fp2_t u2 = fp2_sqr(u);
-  fp2_t zu2 = fp2_mul(Z, u2);
-  fp2_t den = fp2_add(fp2_sqr(zu2), zu2);
   const bool den0 = fp2_is_zero(den);
-  fp2_t x1 = fp2_mul(mba, fp2_add(fp2_one(), fp2_inv(den)));
+  fp2_t x1 = fp2_mul(mba, fp2_add(fp2_one(), den_inv));
   x1 = fp2_select(den0, x1, bza);
   fp2_t gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
   fp2_t r;
@@ -233,6 +239,13 @@ BGV_NOINLINE void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   *xo = x;
   *yo = y;
+}
+
+// returns the SWU point on E2' in affine coordinates
+BGV_NOINLINE void sswu_g2(fp2_t* xo, fp2_t* yo, const fp2_t& u, const fp_t& sqrt_m5) {
+  fp2_t zu2;
+  const fp2_t den = sswu_den(u, &zu2);
+  sswu_finish(xo, yo, u, zu2, den, fp2_inv(den), sqrt_m5);
 }
 
 // 3-isogeny E2' -> E2 (RFC 9380 E.3), output Jacobian without inversion.
@@ -254,15 +267,24 @@ BGV_NOINLINE g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
   return r;
 }
 
-// Full hash_to_G2 of one message: returns Jacobian point in G2.
+// Full hash_to_G2 of one message: returns Jacobian point in G2.  The two maps' 1/den
+// come from one inversion of den0 den1 (a zero den only ever meets the exceptional case,
+// which ignores its inverse; the other map's inverse then comes from its own inversion).
 BGV_NOINLINE g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, len);
   const fp_t sm5 = fp_sqrt_minus5();
+  fp2_t zu0, zu1;
+  const fp2_t d0 = sswu_den(u0, &zu0), d1 = sswu_den(u1, &zu1);
+  const bool z0 = fp2_is_zero(d0), z1 = fp2_is_zero(d1);
+  // 1/(d0 d1) with a zero factor replaced by 1
+  const fp2_t e0 = fp2_select(z0, d0, fp2_one()), e1 = fp2_select(z1, d1, fp2_one());
+  const fp2_t inv = fp2_inv(fp2_mul(e0, e1));
+  const fp2_t i0 = fp2_mul(inv, e1), i1 = fp2_mul(inv, e0);
   fp2_t x, y;
-  sswu_g2(&x, &y, u0, sm5);
+  sswu_finish(&x, &y, u0, zu0, d0, i0, sm5);
   g2_jac q0 = iso_map_g2(x, y);
-  sswu_g2(&x, &y, u1, sm5);
+  sswu_finish(&x, &y, u1, zu1, d1, i1, sm5);
   g2_jac q1 = iso_map_g2(x, y);
   return g2_clear_cofactor(jac_add(q0, q1));
 }

@@ -5,10 +5,25 @@
 #pragma once
 #include "bls_curve.h"
 
+// The G1 point of a Miller loop in Jacobian form P = (X : Y : Z) (no inversion after
+// r_i * pk_i): every line is scaled by Z^3, an Fp factor the final exponentiation kills,
+// so xP = X / Z^2 enters as X Z, yP = Y / Z^3 as Y, and the P-free term as l0 Z^3.
+struct miller_p {
+  fp_t xn;   // -X Z
+  fp_t yp;   // Y
+  fp_t zp3;  // Z^3
+};
+BGV_HD miller_p miller_p_make(const g1_jac& p) {
+  return miller_p{fp_neg(fp_mul(p.x, p.z)), p.y, fp_mul(fp_sqr(p.z), p.z)};
+}
+BGV_HD miller_p miller_p_aff(const g1_aff& p) { return miller_p{fp_neg(p.x), p.y, fp_one()}; }
+
 // Doubling step: T <- 2T; returns the tangent line at T evaluated at P,
 // scaled by Fp2/Fp4 factors that the final exponentiation kills:
-//   l0 = 3X^3 - 2Y^2,  l1 = -3X^2 Z^2 xP,  l3 = Z3 Z^2 yP
-BGV_MILLER_ATTR void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const fp_t& xp_neg, const fp_t& yp) {
+//   l0 = (3X^3 - 2Y^2) Z_P^3,  l1 = -3X^2 Z^2 X_P Z_P,  l3 = Z3 Z^2 Y_P
+BGV_MILLER_ATTR void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const miller_p& P) {
+  const fp_t& xp_neg = P.xn;
+  const fp_t& yp = P.yp;
   fp2_t A = fp2_sqr(t.x);
   fp2_t B = fp2_sqr(t.y);
   fp2_t C = fp2_sqr(B);
@@ -16,7 +31,7 @@ BGV_MILLER_ATTR void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, cons
   fp2_t D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.x, B)), A), C));
   fp2_t E = fp2_add(fp2_dbl(A), A);
   fp2_t F = fp2_sqr(E);
-  *l0 = fp2_sub(fp2_mul(E, t.x), fp2_dbl(B));
+  *l0 = fp2_mul_fp(fp2_sub(fp2_mul(E, t.x), fp2_dbl(B)), P.zp3);
   *l1 = fp2_mul_fp(fp2_mul(E, ZZ), xp_neg);
   fp2_t X3 = fp2_sub(F, fp2_dbl(D));
   fp2_t Y3 = fp2_sub(fp2_mul(E, fp2_sub(D, X3)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
@@ -30,7 +45,7 @@ BGV_MILLER_ATTR void miller_dbl(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, cons
 // Addition step: T <- T + Q (Q affine); returns the chord line at P:
 //   l0 = r xQ - yQ Z3,  l1 = -r xP,  l3 = Z3 yP   (r = 2(S2 - Y))
 BGV_MILLER_ATTR void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, const g2_aff& q, const fp_t& xp_neg,
-                       const fp_t& yp) {
+                       const fp_t& yp) {  // P affine (Z_P = 1)
   fp2_t ZZ = fp2_sqr(t.z);
   fp2_t U2 = fp2_mul(q.x, ZZ);
   fp2_t S2 = fp2_mul(q.y, fp2_mul(t.z, ZZ));
@@ -56,12 +71,13 @@ BGV_MILLER_ATTR void miller_add(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, cons
 BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
   const fp_t xp_neg = fp_neg(p.x);
   const fp_t yp = p.y;
+  const miller_p P = miller_p_aff(p);
   g2_jac t = jac_from_aff(q);
   fp12_t f = fp12_one();
   fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
   // first doubling: f = 1, so f^2 * line = line
-  miller_dbl(t, &l0, &l1, &l3, xp_neg, yp);
+  miller_dbl(t, &l0, &l1, &l3, P);
   f = fp12_mul_line(f, l0, l1, l3);
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
@@ -69,7 +85,7 @@ BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
       f = fp12_mul_line(f, l0, l1, l3);
     }
     f = fp12_sqr(f);
-    miller_dbl(t, &l0, &l1, &l3, xp_neg, yp);
+    miller_dbl(t, &l0, &l1, &l3, P);
     f = fp12_mul_line(f, l0, l1, l3);
   }
   // bit 0 of |x| is 0: no trailing addition
@@ -77,22 +93,24 @@ BGV_NOINLINE fp12_t miller_loop(const g1_aff& p, const g2_aff& q) {
 }
 
 // Addition step with a Jacobian Q = (X2 : Y2 : Z2) (no affine conversion of Q):
-// T <- T + Q, and the chord line at P scaled by Z2^3 (an Fp2 factor, killed by the
-// final exponentiation):  l0 = r X2 Z2 - Y2 Z3,  l1 = -r Z2^3 xP,  l3 = Z3 Z2^3 yP.
-// q.zz = Z2^2, q.zzz_xn = -Z2^3 xP, q.zzz_yp = Z2^3 yP, q.xz = X2 Z2 are per-pair constants.
+// T <- T + Q, and the chord line at P scaled by Z2^3 (an Fp2 factor) and Z_P^3 (Fp), both
+// killed by the final exponentiation:  l0 = (r X2 Z2 - Y2 Z3) Z_P^3,  l1 = -r Z2^3 X_P Z_P,
+// l3 = Z3 Z2^3 Y_P.  Per-pair constants: q.zz = Z2^2, q.xz = X2 Z2 Z_P^3, q.y2z = Y2 Z_P^3,
+// q.zzz_xn = -Z2^3 X_P Z_P, q.zzz_yp = Z2^3 Y_P.
 struct miller_jq {
   g2_jac q;
-  fp2_t zz, xz, zzz_xn, zzz_yp;
+  fp2_t zz, xz, y2z, zzz_xn, zzz_yp;
 };
 
-BGV_HD miller_jq miller_jq_make(const g2_jac& q, const fp_t& xp_neg, const fp_t& yp) {
+BGV_HD miller_jq miller_jq_make(const g2_jac& q, const miller_p& P) {
   miller_jq r;
   r.q = q;
   r.zz = fp2_sqr(q.z);
   const fp2_t zzz = fp2_mul(r.zz, q.z);
-  r.xz = fp2_mul(q.x, q.z);
-  r.zzz_xn = fp2_mul_fp(zzz, xp_neg);
-  r.zzz_yp = fp2_mul_fp(zzz, yp);
+  r.xz = fp2_mul_fp(fp2_mul(q.x, q.z), P.zp3);
+  r.y2z = fp2_mul_fp(q.y, P.zp3);
+  r.zzz_xn = fp2_mul_fp(zzz, P.xn);
+  r.zzz_yp = fp2_mul_fp(zzz, P.yp);
   return r;
 }
 
@@ -111,7 +129,7 @@ BGV_MILLER_ATTR void miller_add_jq(g2_jac& t, fp2_t* l0, fp2_t* l1, fp2_t* l3, c
   fp2_t X3 = fp2_sub(fp2_sub(fp2_sqr(r), J), fp2_dbl(V));
   fp2_t Y3 = fp2_sub(fp2_mul(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul(S1, J)));
   fp2_t Z3 = fp2_mul(fp2_sub(fp2_sub(fp2_sqr(fp2_add(t.z, c.q.z)), ZZ), c.zz), H);
-  *l0 = fp2_sub(fp2_mul(r, c.xz), fp2_mul(c.q.y, Z3));
+  *l0 = fp2_sub(fp2_mul(r, c.xz), fp2_mul(c.y2z, Z3));
   *l1 = fp2_mul(r, c.zzz_xn);
   *l3 = fp2_mul(Z3, c.zzz_yp);
   t.x = X3;
@@ -128,32 +146,32 @@ BGV_HD fp12_t fp12_from_line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) 
   return fp12_t{fp6_t{l0, l1, fp2_zero()}, fp6_t{fp2_zero(), l3, fp2_zero()}};
 }
 
-// f_{|x|,Q}(P) for ONE pair (conjugated for x < 0): P affine, Q Jacobian (Z != 0).
+// f_{|x|,Q}(P) for ONE pair (conjugated for x < 0): P and Q Jacobian (Z != 0).
 // The per-set Miller loop of the blst batch equation (maybeBatch.ts:18-25 ->
 // verifyMultipleAggregateSignatures): e(r_i pk_i, H(m_i)); the signature side
 // e(-G1, sum r_i sig_i) is one team loop per device group (bls_team.h).
-BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_aff& p, const g2_jac& q) {
-  const fp_t xn = fp_neg(p.x);
+BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) {
+  const miller_p P = miller_p_make(p);
 #ifndef BGV_MILLER_JQ_RECOMPUTE
-  const miller_jq c = miller_jq_make(q, xn, p.y);
+  const miller_jq c = miller_jq_make(q, P);
 #endif
   g2_jac t = q;
   fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
-  miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+  miller_dbl(t, &l0, &l1, &l3, P);
   fp12_t f = fp12_from_line(l0, l1, l3);
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
 #ifdef BGV_MILLER_JQ_RECOMPUTE
       // the Jacobian-Q constants for the 5 addition steps only: 112 fewer live VGPRs
       // across the 63 doubling steps, 5 x 17 Fp products recomputed
-      const miller_jq c = miller_jq_make(q, xn, p.y);
+      const miller_jq c = miller_jq_make(q, P);
 #endif
       miller_add_jq(t, &l0, &l1, &l3, c);
       f = fp12_mul_line(f, l0, l1, l3);
     }
     f = fp12_sqr(f);
-    miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+    miller_dbl(t, &l0, &l1, &l3, P);
     f = fp12_mul_line(f, l0, l1, l3);
   }
   return fp12_conj(f);

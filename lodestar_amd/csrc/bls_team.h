@@ -187,16 +187,16 @@ BGV_HD fp_t tm_mul_line_lane(int c, const fp_t* A, const fp2_t& l0, const fp2_t&
 
 // f_{|x|,Q}(P), conjugated (x < 0), with f held by a team: the twist point T and the
 // lines are computed by every lane of the team (lane-uniform control flow), the Fp12
-// accumulator is coefficient-parallel (O::sqr, O::mul_line).  P affine, Q Jacobian and
+// accumulator is coefficient-parallel (O::sqr, O::mul_line).  P and Q Jacobian and
 // finite.  Same steps and lines as miller_loop1 (bls_pairing.h), so the value is equal.
 template <class E, class O>
-BGV_HD E tm_miller_loop(O& o, const g1_aff& p, const g2_jac& q) {
-  const fp_t xn = fp_neg(p.x);
-  const miller_jq cq = miller_jq_make(q, xn, p.y);
+BGV_HD E tm_miller_loop(O& o, const g1_jac& p, const g2_jac& q) {
+  const miller_p P = miller_p_make(p);
+  const miller_jq cq = miller_jq_make(q, P);
   g2_jac t = q;
   fp2_t l0, l1, l3;
   const uint64_t X = BGV_X_ABS;
-  miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+  miller_dbl(t, &l0, &l1, &l3, P);
   E f = o.line(l0, l1, l3);
   BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
     if ((X >> (i + 1)) & 1) {
@@ -204,7 +204,7 @@ BGV_HD E tm_miller_loop(O& o, const g1_aff& p, const g2_jac& q) {
       f = o.mul_line(f, l0, l1, l3);
     }
     f = o.sqr(f);
-    miller_dbl(t, &l0, &l1, &l3, xn, p.y);
+    miller_dbl(t, &l0, &l1, &l3, P);
     f = o.mul_line(f, l0, l1, l3);
   }
   return o.conj(f);

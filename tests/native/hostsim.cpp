@@ -59,14 +59,15 @@ int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_aff p = in_g1(pk_aff_tl);
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
-  g1_aff pa;
-  return jac_to_aff(&pa, jac_mul_u64(acc, r));
+  return !jac_is_inf(jac_mul_u64(acc, r));  // Jacobian: the Miller loop takes P projectively
 }
 void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
-  (void)miller_loop1(in_g1(p), jac_from_aff(in_g2(q)));
+  (void)miller_loop1(jac_from_aff(in_g1(p)), jac_from_aff(in_g2(q)));
 }
 // the group's signature pair e(-G1, sum r_i sig_i), counted as the one-lane loop
-void hs_k_group_miller_body(const uint8_t* q) { (void)miller_loop1(g1_neg_generator(), jac_from_aff(in_g2(q))); }
+void hs_k_group_miller_body(const uint8_t* q) {
+  (void)miller_loop1(jac_from_aff(g1_neg_generator()), jac_from_aff(in_g2(q)));
+}
 // one complete G2 addition of the group's signature sum
 void hs_k_group_add_body(const uint8_t* q, const uint8_t* q2) {
   (void)jac_add(jac_from_aff(in_g2(q)), jac_from_aff(in_g2(q2)));
@@ -215,17 +216,23 @@ static g2_jac jac_scaled(const g2_aff& a) {
   const fp2_t l2 = fp2_sqr(l);
   return g2_jac{fp2_mul(a.x, l2), fp2_mul(a.y, fp2_mul(l2, l)), l};
 }
+// P handed over in Jacobian form with Z != 1 as well: (l^2 x, l^3 y, l), l = 7
+static g1_jac g1_scaled(const g1_aff& a) {
+  const fp_t l = fp_to_mont(fp_t{{7}});
+  const fp_t l2 = fp_sqr(l);
+  return g1_jac{fp_mul(a.x, l2), fp_mul(a.y, fp_mul(l2, l)), l};
+}
 void hs_miller_loop1(uint8_t* out, const uint8_t* p, const uint8_t* q) {
-  out_fp12(out, miller_loop1(in_g1(p), jac_scaled(in_g2(q))));
+  out_fp12(out, miller_loop1(g1_scaled(in_g1(p)), jac_scaled(in_g2(q))));
 }
 // the team Miller loop of k_final (bls_team.h tm_miller_loop), emulated lane by lane
 void hs_team_miller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
   tm_emu_ops o;
-  out_fp12(out, tm_emu_to_fp12(tm_miller_loop<tm_emu_t>(o, in_g1(p), jac_scaled(in_g2(q)))));
+  out_fp12(out, tm_emu_to_fp12(tm_miller_loop<tm_emu_t>(o, g1_scaled(in_g1(p)), jac_scaled(in_g2(q)))));
 }
 // the latency path's team loop (bgv_tmiller.h: table-driven twist-point rounds + team Fp12)
 void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
-  out_fp12(out, tm_team_miller_host(in_g1(p), jac_scaled(in_g2(q))));
+  out_fp12(out, tm_team_miller_host(g1_scaled(in_g1(p)), jac_scaled(in_g2(q))));
 }
 void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   tm_emu_ops o;
@@ -234,12 +241,12 @@ void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uin
 // one set through the device equation: k_prep (r pk affine, r sig Jacobian), k_miller
 // (e(r pk, H)), the group's team loop e(-G1, r sig), the product and the team final check
 int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* sig_aff, uint64_t r) {
-  g1_aff pa;
-  if (!jac_to_aff(&pa, jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r))) return 0;
+  const g1_jac pa = jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r);
+  if (jac_is_inf(pa)) return 0;
   const g2_jac rs = jac_mul_u64(jac_from_aff(in_g2(sig_aff)), r);
   tm_emu_ops o;
   const tm_emu_t f = tm_emu_from_fp12(miller_loop1(pa, jac_from_aff(in_g2(h_aff))));
-  const tm_emu_t g = tm_miller_loop<tm_emu_t>(o, g1_neg_generator(), rs);
+  const tm_emu_t g = tm_miller_loop<tm_emu_t>(o, jac_from_aff(g1_neg_generator()), rs);
   return tm_final_exp_is_one(o, o.mul(f, g));
 }
 

@@ -27,15 +27,17 @@ MAX_TERMS = 8      # products per instruction (column sums < 2^63 for limbs < 2^
 MAX_LIN = 6        # slots per lin()
 
 # ---- fixed slots --------------------------------------------------------------------------
-ONE, XN, YP = 0, 1, 2                       # Montgomery 1, -xP, yP
+ONE, XN, YP = 0, 1, 2                       # Montgomery 1, -X_P Z_P, Y_P (P Jacobian)
 QX, QY, QZ = (3, 4), (5, 6), (7, 8)         # Q (Jacobian)
 ZZ, XZ, ZZZ, ZZZ_XN, ZZZ_YP = (9, 10), (11, 12), (13, 14), (15, 16), (17, 18)
 BANK = [((19, 20), (21, 22), (23, 24)), ((25, 26), (27, 28), (29, 30))]  # T = (X, Y, Z)
 L0, L1, L3 = (31, 32), (33, 34), (35, 36)   # the step's line
 DUMMY = 37
-TEMP0 = 38
+ZP3 = 38                                    # Z_P^3 (lines scaled by it, bls_pairing.h miller_p)
+Y2S = (39, 40)                              # Y2 Z_P^3
+TEMP0 = 41
 
-INPUT_BOUND = {ONE: 1, XN: 2, YP: 2}
+INPUT_BOUND = {ONE: 1, XN: 2, YP: 2, ZP3: 2}
 for s in QX + QY + QZ:
     INPUT_BOUND[s] = 2
 
@@ -153,9 +155,11 @@ def prog_init():
     g = Prog("init", INPUT_BOUND)
     Q = {"x": pair(QX), "y": pair(QY), "z": pair(QZ)}
     zz = g.sqr2(Q["z"], out=ZZ)
-    xz = g.mul2(Q["x"], Q["z"], out=XZ)
+    xz = g.mul2(Q["x"], Q["z"])
+    g.mulfp(Q["y"], S(ZP3), out=Y2S)
     g.new_round()
     zzz = g.mul2(zz, Q["z"], out=ZZZ)
+    g.mulfp(xz, S(ZP3), out=XZ)
     g.new_round()
     g.mulfp(zzz, S(XN), out=ZZZ_XN)
     g.mulfp(zzz, S(YP), out=ZZZ_YP)
@@ -164,7 +168,7 @@ def prog_init():
 
 def base_bounds(src_bank, init):
     b = dict(INPUT_BOUND)
-    for s in ZZ + XZ + ZZZ + ZZZ_XN + ZZZ_YP:
+    for s in ZZ + XZ + ZZZ + ZZZ_XN + ZZZ_YP + Y2S:
         b[s] = init.bound[s]
     for t in BANK[src_bank]:
         for s in t:
@@ -188,8 +192,7 @@ def prog_dbl(src, init, bank_bound):
     G = g.sqr2(lin2((1, X), (1, B)))
     F = g.sqr2(lin2((3, A)))
     E = lin2((3, A))
-    negB2 = lin2((-2, B))
-    g.mul2(E, X, out=L0, extra=([(negB2[0], S(ONE))], [(negB2[1], S(ONE))]))
+    EX = g.mul2(E, X)
     EZZ = g.mul2(E, ZZl)
     Z3ZZ = g.mul2(Z3, ZZl)
     g.new_round()
@@ -202,6 +205,7 @@ def prog_dbl(src, init, bank_bound):
     g.mul2(E, DmX3, out=Y3o, extra=([(negC8[0], S(ONE))], [(negC8[1], S(ONE))]))
     g.mulfp(EZZ, S(XN), out=L1)
     g.mulfp(Z3ZZ, S(YP), out=L3)
+    g.mulfp(lin2((1, EX), (-2, B)), S(ZP3), out=L0)   # (E X - 2B) Z_P^3
     del D
     return g
 
@@ -231,11 +235,13 @@ def prog_add(src, init, bank_bound):
     rr = g.sqr2(r)
     Z3 = g.mul2(Z3p, H, out=Z3o)
     g.new_round()
-    # R4: J = H I = 4 H HH, V = U1 I = 4 U1 HH, l0 = r xz - Y2 Z3, l1 = r zzz_xn, l3 = Z3 zzz_yp
+    # R4: J = H I = 4 H HH, V = U1 I = 4 U1 HH, l0 = r xz - Y2 Z3 (xz, Y2 scaled by Z_P^3),
+    # l1 = r zzz_xn, l3 = Z3 zzz_yp
     J = g.mul2(lin2((4, H)), HH)
     V = g.mul2(lin2((4, U1)), HH)
-    nY2 = lin2((-1, q["y"]))
-    g.mul2(r, xz, out=L0, extra=([(nY2[0], Z3[0]), (q["y"][1], Z3[1])],
+    y2s = pair(Y2S)
+    nY2 = lin2((-1, y2s))
+    g.mul2(r, xz, out=L0, extra=([(nY2[0], Z3[0]), (y2s[1], Z3[1])],
                                  [(nY2[0], Z3[1]), (nY2[1], Z3[0])]))
     g.mul2(r, zzz_xn, out=L1)
     g.mul2(Z3, zzz_yp, out=L3)
@@ -293,7 +299,7 @@ def emit(progs):
         lines.append("#define TMP_%s %d" % (name.upper(), off))
     for name, val in (("ONE", ONE), ("XN", XN), ("YP", YP), ("QX", QX[0]), ("QY", QY[0]), ("QZ", QZ[0]),
                       ("BANK0", BANK[0][0][0]), ("BANK1", BANK[1][0][0]), ("L0", L0[0]), ("L1", L1[0]),
-                      ("L3", L3[0]), ("DUMMY", DUMMY)):
+                      ("L3", L3[0]), ("DUMMY", DUMMY), ("ZP3", ZP3)):
         lines.append("#define TMP_S_%s %d" % (name, val))
     lines.append("#define TMP_TABLE_BYTES %d" % len(table))
     body = ",".join(str(b) for b in table)
