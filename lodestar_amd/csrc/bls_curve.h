@@ -208,21 +208,36 @@ BGV_HD bool jac_eq(const jac_t<F>& p, const jac_t<F>& q) {
   return (pi && qi) || (!pi && !qi && ex && ey);
 }
 
+// An index the compiler cannot fold (always 0): reading a point through tab[bgv_opaque0()]
+// keeps it in (scratch) memory, read where it is used, instead of live in registers across
+// a loop that has no room for it -- in which case the allocator spills it on every
+// iteration (k_prep: ~650 KB of scratch traffic per set before, tools/gpu notes in DESIGN).
+BGV_HD int bgv_opaque0() {
+  int z = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(z));
+#else
+  asm volatile("" : "+r"(z));
+#endif
+  return z;
+}
+
 // [k]P for a 64-bit (lane-varying) scalar: left-to-right, 2-bit fixed window
 // with a 3-entry table; the add is computed in every lane and selected, so a
-// wave never diverges on scalar bits.
+// wave never diverges on scalar bits.  The table lives in memory and one entry is
+// loaded per window (the accumulator and the addition's temporaries fill the registers).
 template <class F>
 BGV_NOINLINE jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
-  jac_t<F> t1 = p;
-  jac_t<F> t2 = jac_dbl(p);
-  jac_t<F> t3 = jac_add(t2, p);
+  jac_t<F> tab[4];
+  tab[1] = p;
+  tab[2] = jac_dbl(p);
+  tab[3] = jac_add(tab[2], p);
+  tab[0] = tab[1];
   jac_t<F> acc = jac_infinity<F>();
   BGV_NO_UNROLL for (int i = 62; i >= 0; i -= 2) {
     acc = jac_dbl(jac_dbl(acc));
     const uint32_t d = (uint32_t)(k >> i) & 3u;
-    jac_t<F> s = jac_select(d == 2u, t1, t2);
-    s = jac_select(d == 3u, s, t3);
-    jac_t<F> sum = jac_add(acc, s);
+    const jac_t<F> sum = jac_add(acc, tab[d]);
     acc = jac_select(d != 0u, acc, sum);
   }
   return acc;
@@ -232,29 +247,32 @@ BGV_NOINLINE jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
 // the keygen/sign utilities), same 2-bit fixed window as jac_mul_u64.
 template <class F>
 BGV_NOINLINE jac_t<F> jac_mul_u256(const jac_t<F>& p, const uint32_t k[8]) {
-  jac_t<F> t1 = p;
-  jac_t<F> t2 = jac_dbl(p);
-  jac_t<F> t3 = jac_add(t2, p);
+  jac_t<F> tab[4];
+  tab[1] = p;
+  tab[2] = jac_dbl(p);
+  tab[3] = jac_add(tab[2], p);
+  tab[0] = tab[1];
   jac_t<F> acc = jac_infinity<F>();
   BGV_NO_UNROLL for (int i = 254; i >= 0; i -= 2) {
     acc = jac_dbl(jac_dbl(acc));
     const uint32_t d = (k[i >> 5] >> (i & 31)) & 3u;
-    jac_t<F> s = jac_select(d == 2u, t1, t2);
-    s = jac_select(d == 3u, s, t3);
-    jac_t<F> sum = jac_add(acc, s);
+    const jac_t<F> sum = jac_add(acc, tab[d]);
     acc = jac_select(d != 0u, acc, sum);
   }
   return acc;
 }
 
-// [|x|]P, |x| = 0xd201000000010000 (lane-uniform bits: no divergence)
+// [|x|]P, |x| = 0xd201000000010000 (lane-uniform bits: no divergence).  P is read from
+// memory at the 5 additions; the 63 doublings keep only the accumulator live.
 template <class F>
 BGV_NOINLINE jac_t<F> jac_mul_x_abs(const jac_t<F>& p) {
+  jac_t<F> pm[1];
+  pm[0] = p;
   jac_t<F> acc = p;
   const uint64_t X = BGV_X_ABS;
   BGV_NO_UNROLL for (int i = 62; i >= 0; --i) {
     acc = jac_dbl(acc);
-    if ((X >> i) & 1) acc = jac_add(acc, p);
+    if ((X >> i) & 1) acc = jac_add(acc, pm[bgv_opaque0()]);
   }
   return acc;
 }
