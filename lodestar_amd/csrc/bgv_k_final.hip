@@ -48,6 +48,41 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
   if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
+// The latency path's closing (small calls): one block of 4 teams per group.  Team t
+// multiplies the group's slots t, t + 4, ... (team 0 also the signature pair), the four
+// partial products meet in LDS and every team forms the same product in the same order
+// and runs the final-exponentiation check on it (team 0 reports).  A quarter of k_final's
+// serial product chain; the check is unchanged.
+__global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                       const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
+                                       int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod) {
+  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
+  __shared__ fp_t part[BGV_FINAL_TEAMS][BGV_TEAM_COMPS];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
+  const uint32_t gi = blockIdx.x;
+  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  const int fi = tm_fp_index(cc);
+  const fp_t one_c = cc == 0 ? fp_one() : fp_zero();
+  tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
+  const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
+  constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
+  fp_t x = team == 0 ? reinterpret_cast<const fp_t*>(gpair + (gi < ngroups ? gi : ngroups - 1))[fi] : one_c;
+  const uint32_t nmax = (g.n_slots + BGV_FINAL_TEAMS - 1) / BGV_FINAL_TEAMS;
+  BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
+    const uint32_t idx = team + BGV_FINAL_TEAMS * k;
+    const fp_t y = idx < g.n_slots ? fs[kFp12 * idx + fi] : one_c;
+    x = o.mul(x, y);
+  }
+  if (c < BGV_TEAM_COMPS) part[team][cc] = x;
+  __syncthreads();
+  x = part[0][cc];
+  BGV_UNROLL for (int t = 1; t < BGV_FINAL_TEAMS; ++t) x = o.mul(x, part[t][cc]);
+  if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
+  const bool one = tm_final_exp_is_one(o, x);
+  if (gi < ngroups && team == 0 && c == 0) verdict[gi] = one ? 1 : 0;
+}
+
 // Products of runs of Fp12 values (cross-process partials): team t of the
 // grid multiplies in[t * chunk, min(n, (t + 1) * chunk)) into out[t] (1 for an empty run).
 // Teams of a wave loop to the wave's longest run, multiplying by 1, so every lane reaches
@@ -114,8 +149,12 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     const hipError_t e = bgv_launch_gpairs(b, s.main);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
-                     b.f, b.gpair, b.verdict, b.gprod);
+  if (b.nslots + b.ngroups <= bgv_latency_max())
+    hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
+                       b.verdict, b.gprod);
+  else
+    hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
+                       b.f, b.gpair, b.verdict, b.gprod);
   BGV_MARK(5);
   return hipGetLastError();
 }

@@ -14,6 +14,47 @@
 //              hash hash_to_G2(signing root) -> H(m_i), Jacobian
 //              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i (Jacobian)
 #include "bgv_device.h"
+#include "bgv_team_dev.h"
+#include "bgv_tcurve.h"
+
+static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
+
+// Device engine of the team G2 schedules (bgv_tcurve.h): programs over the team's LDS slots
+// with a block barrier per round; every team of the block runs the same sequence.
+struct tc_dev_engine {
+  const uint8_t* prog;
+  fp_t* S;
+  int c;
+  bool bad;
+  __device__ void run(int off) {
+    int pos = off;
+    const int nr = prog[pos++];
+    for (int r = 0; r < nr; ++r) {
+      const int T = prog[pos], M = prog[pos + 1];
+      pos += 2;
+      const int rb = tmp_rec_bytes(T, M);
+      int out;
+      const fp_t v = tmp_lane(S, prog + pos + c * rb, T, M, &out);
+      S[out] = v;  // no slot is read and written in one round (tools/gen_tcurve.py)
+      __syncthreads();
+      pos += BGV_TEAM * rb;
+    }
+  }
+  __device__ void copy(int dst, int src) {  // src may differ per team (a digit's table entry)
+    if (c < 6 && dst != src) S[TCP_BANK(dst) + c] = S[TCP_BANK(src) + c];
+    __syncthreads();
+  }
+  __device__ void neg_y(int b) {
+    if (c == 2 || c == 3) S[TCP_BANK(b) + c] = fp_neg(S[TCP_BANK(b) + c]);
+    __syncthreads();
+  }
+  __device__ void check_add() {
+    if (c == 0) {
+      const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
+      bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+    }
+  }
+};
 
 extern "C" {
 
@@ -219,6 +260,69 @@ __global__ void BGV_KATTR_PREP k_prep_b(const bgv_dslot* __restrict__ slots, uin
   }
 }
 
+// The latency path's second launch on teams (bgv_tcurve.h): blockIdx.y = 0 the cofactor
+// clearing of q0 + q1 (one team per set), 1 r_i * sig_i (one team per set), 2 the
+// signature's subgroup check (one lane per set).  A team whose cofactor clearing met an
+// exceptional addition recomputes it on one lane with the complete formulas.
+__global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                  g2_jac* __restrict__ h, fp12_t* __restrict__ f,
+                                                  g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status) {
+  if (blockIdx.y == 2) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots || (slots[s].flags & BGV_SLOT_PAD) || sig_status[s] != BGV_ST_OK) return;
+    if (!g2_in_subgroup(jac_from_aff(*split_sig(f, s)))) sig_status[s] = BGV_POINT_NOT_IN_GROUP;
+    return;
+  }
+  __shared__ uint8_t prog[TCP_TABLE_BYTES];
+  __shared__ fp_t Sall[BGV_FINAL_TEAMS][TCP_NSLOT];
+  __shared__ int flags[BGV_FINAL_TEAMS];
+  for (int i = threadIdx.x; i < TCP_TABLE_BYTES; i += 64) prog[i] = kTcProg[i];
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const uint32_t u = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const uint32_t uu = u < nslots ? u : nslots - 1;
+  const bgv_dslot& d = slots[uu];
+  const bool real = u < nslots && !(d.flags & BGV_SLOT_PAD);
+  fp_t* S = Sall[team];
+  if (c == 6) {
+    S[TCP_S_ONE] = fp_one();
+  } else if (c >= 7 && c < 11) {
+    const fp2_t cx = BGV_PSI_CX, cy = BGV_PSI_CY;
+    const fp2_t& v = c < 9 ? cx : cy;
+    S[c < 9 ? TCP_S_PSI_CX + (c - 7) : TCP_S_PSI_CY + (c - 9)] = (c & 1) ? v.c0 : v.c1;
+  } else if (c == 11) {
+    S[TCP_S_PSI2_CX] = fp_t{BGV_PSI2_CX};
+  } else if (c == 12) {
+    S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
+  }
+  tc_dev_engine e{prog, S, c, false};
+  if (blockIdx.y == 0) {
+    if (c < 6) {
+      S[TCP_BANK(1) + c] = reinterpret_cast<const fp_t*>(h + uu)[c];
+      S[TCP_BANK(2) + c] = reinterpret_cast<const fp_t*>(split_q1(f, uu))[c];
+    }
+    __syncthreads();
+    tc_clear_cofactor(e);
+    if (c == 0) flags[team] = e.bad ? 1 : 0;
+    __syncthreads();
+    if (real) {
+      if (!flags[team]) {
+        if (c < 6) reinterpret_cast<fp_t*>(h + uu)[c] = S[TCP_BANK(3) + c];
+      } else if (c == 0) {
+        h[uu] = g2_clear_cofactor(jac_add(h[uu], *split_q1(f, uu)));
+      }
+    }
+  } else {
+    const bool ok = sig_status[uu] == BGV_ST_OK;  // the decode left it OK (the subgroup lanes may flip it)
+    if (c < 4)
+      S[TCP_BANK(1) + c] = reinterpret_cast<const fp_t*>(split_sig(f, uu))[c];
+    else if (c < 6)
+      S[TCP_BANK(1) + c] = c == 4 ? fp_one() : fp_zero();
+    __syncthreads();
+    tc_mul_u64(e, d.scalar);
+    if (real && ok && c < 6) reinterpret_cast<fp_t*>(rsig + uu)[c] = S[TCP_BANK(4) + c];
+  }
+}
+
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
@@ -268,8 +372,8 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
     hipLaunchKernelGGL(k_prep_a, dim3(nblk(n, 64), 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
                        tree ? b.pk_agg : nullptr);
-    hipLaunchKernelGGL(k_prep_b, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig,
-                       b.sig_status);
+    hipLaunchKernelGGL(k_prep_team, dim3(nblk(n, BGV_FINAL_TEAMS), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f,
+                       b.rsig, b.sig_status);
   } else {
     hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,

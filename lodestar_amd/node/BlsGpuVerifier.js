@@ -21,13 +21,15 @@ const path = require("path");
 const addon = require(path.join(__dirname, "blsgpu.node"));
 
 const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:39
-// Batchable buffering (index.ts:48,57 use 32 sets / 100 ms for CPU workers).  One device call
-// verifies up to ~163k sets in the time of a few hundred, so the GPU wants every set the
-// gossip queues hold (<= 64 concurrent validations each, network/gossip/validation/queue.ts:14)
-// in as few calls as possible: flush at 1024 buffered sets or after 20 ms, and let the
-// library's dispatchers merge the calls that are in flight together (DESIGN.md §3).
-const MAX_BUFFERED_SIGS = 1024;
-const MAX_BUFFER_WAIT_MS = 20;
+// Batchable buffering (index.ts:48,57 use 32 sets / 100 ms for CPU workers).  Gossip caps
+// concurrency per topic (64 for attestations, network/gossip/validation/queue.ts:14), so the
+// Node-level rate is concurrency / per-call latency: a long buffer wait only adds latency,
+// and the library already merges the calls in flight into super-batches.  Measured with 64
+// concurrent one-set callers on one MI355X (tests/node/gossip_bench.js,
+// profiles/r02/gossip_node_64callers_t6.jsonl): 32 sets / 100 ms 1.35k sets/s, 32 / 2 ms
+// 5.2k, 64 / 1 ms 5.7k sets/s at p50 11 ms.
+const MAX_BUFFERED_SIGS = 64;
+const MAX_BUFFER_WAIT_MS = 1;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
 

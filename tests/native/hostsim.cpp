@@ -10,6 +10,7 @@
 #include "../../lodestar_amd/csrc/bls_pairing.h"
 #include "../../lodestar_amd/csrc/bls_team.h"
 #include "../../lodestar_amd/csrc/bgv_tmiller.h"
+#include "../../lodestar_amd/csrc/bgv_tcurve.h"
 
 static fp_t in_fp(const uint8_t* be) { return fp_to_mont(fp_from_be48(be)); }
 static void out_fp(uint8_t* be, const fp_t& a) { fp_to_be48(be, fp_from_mont(a)); }
@@ -229,6 +230,23 @@ void hs_miller_loop1(uint8_t* out, const uint8_t* p, const uint8_t* q) {
 void hs_team_miller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
   tm_emu_ops o;
   out_fp12(out, tm_emu_to_fp12(tm_miller_loop<tm_emu_t>(o, g1_scaled(in_g1(p)), jac_scaled(in_g2(q)))));
+}
+// the latency path's team G2 schedules (bgv_tcurve.h) against the one-lane formulas:
+// returns 1 when both the cofactor clearing of a message's two SSWU points and [k] of the
+// result agree (as affine points), 0 otherwise; *bad_out = the exceptional-addition flag
+int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
+  fp2_t u0, u1, x, y;
+  hash_to_field_fp2(&u0, &u1, msg32, 32);
+  sswu_g2(&x, &y, u0, fp_sqrt_minus5());
+  const g2_jac q0 = iso_map_g2(x, y);
+  sswu_g2(&x, &y, u1, fp_sqrt_minus5());
+  const g2_jac q1 = iso_map_g2(x, y);
+  bool bad;
+  const g2_jac h_team = tc_clear_cofactor_host(q0, q1, &bad);
+  const g2_jac h_lane = g2_clear_cofactor(jac_add(q0, q1));
+  *bad_out = bad;
+  if (!jac_eq(h_team, h_lane)) return 0;
+  return jac_eq(tc_mul_u64_host(h_lane, k), jac_mul_u64(h_lane, k)) ? 1 : 0;
 }
 // the latency path's team loop (bgv_tmiller.h: table-driven twist-point rounds + team Fp12)
 void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {

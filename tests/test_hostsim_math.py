@@ -5,6 +5,7 @@ Every device formula — Montgomery CIOS, Fp2 sqrt, line functions, Miller
 loop, final exponentiation, SSWU/iso/cofactor, ZCash decoding — is checked
 here bit-for-bit before it ever runs on an MI355X.
 """
+import hashlib
 import random
 
 import pytest
@@ -280,6 +281,19 @@ def test_table_driven_team_miller_loop(L):
         L.hs_miller_loop1(m1, hs.g1_b(p), hs.g2_b(q))
         L.hs_tmiller(tm, hs.g1_b(p), hs.g2_b(q))
         assert tm.raw == m1.raw
+
+
+def test_team_g2_schedules(L):
+    """The latency path's team cofactor clearing and r * sig (bgv_tcurve.h, generated point
+    programs, emulated lane by lane) equal g2_clear_cofactor and jac_mul_u64 as points, for
+    random messages and 64-bit scalars (including top digits 0 and a scalar of 1)."""
+    import ctypes
+    for k, m in enumerate((b"a", b"tcurve", b"x" * 7)):
+        msg = hashlib.sha256(m).digest()
+        scalar = (rnd.getrandbits(64) | 1) if k == 0 else (1 if k == 1 else rnd.getrandbits(40) | 1)
+        bad = ctypes.c_int(7)
+        assert L.hs_tcurve_check(msg, ctypes.c_uint64(scalar), ctypes.byref(bad)) == 1
+        assert bad.value == 0
 
 
 def test_team_mul_line(L):
