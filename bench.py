@@ -31,6 +31,7 @@ import os
 import random
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -160,10 +161,13 @@ def block_import_latency(ctx, native, nkeys, runs=100):
             "runs": runs}
 
 
-def aggregate_throughput(ctx, native, nkeys, calls=384, inflight=128):
+def aggregate_throughput(ctx, native, nkeys, calls=1024, inflight=128):
     """config 2: 1024 aggregate sets x 128 distinct cached keys (contiguous committees),
     distinct signing roots, all valid, sent as the pool sends them (8 batchable jobs of
-    128 sets, index.ts:155-166); `calls` such calls, `inflight` at a time."""
+    128 sets, index.ts:155-166); `calls` such calls streaming with `inflight` outstanding.
+    Super-batches hold `inflight` calls (131,072 sets), so completions arrive in bursts of
+    `inflight`: the rate is taken between the end of the 2nd burst and the end of the last
+    (steady state, no pipeline fill or drain inside the window)."""
     from concurrent.futures import ThreadPoolExecutor
     nsets, per = 1024, 128
     assert nsets * per <= nkeys
@@ -175,6 +179,8 @@ def aggregate_throughput(ctx, native, nkeys, calls=384, inflight=128):
             for a in range(nsets)]
     jobs = [(sets[j:j + 128], True) for j in range(0, nsets, 128)]
     packed = native.PackedCall(jobs)
+    done = []
+    lock = threading.Lock()
 
     def call(_):
         out = (native.ctypes.c_int32 * len(jobs))()
@@ -182,20 +188,24 @@ def aggregate_throughput(ctx, native, nkeys, calls=384, inflight=128):
                                 out, None)
         if rc != 0:
             raise native.DeviceError(native.strerror(rc))
+        with lock:
+            done.append(time.perf_counter())
         return list(out)
 
     assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
-    # enough calls in flight to fill whole super-batches (128 x 1024 sets = 131,072)
-    ctx.set_batching(131072, 20000)
-    t0 = time.perf_counter()
+    done.clear()
+    ctx.set_batching(inflight * nsets, 20000)
     with ThreadPoolExecutor(max_workers=inflight) as pool:
         res = list(pool.map(call, range(calls)))
-    dt = time.perf_counter() - t0
     ctx.set_batching(131072, 2000)
     assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
-    return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls, "
-                      "%d in flight" % (calls, inflight),
-            "value": nsets * calls / dt, "unit": "sets/s", "pubkeys_per_s": nsets * per * calls / dt}
+    done.sort()
+    a, b = 2 * inflight - 1, len(done) - 1
+    rate = nsets * (b - a) / (done[b] - done[a])
+    return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls "
+                      "streaming, %d in flight; rate between the 2nd and the last super-batch completion"
+                      % (calls, inflight),
+            "value": rate, "unit": "sets/s", "pubkeys_per_s": rate * per}
 
 
 def host_cpu():

@@ -20,10 +20,14 @@
 #ifndef BGV_WPE_PREP
 #define BGV_WPE_PREP 2
 #endif
-// Sets with at least this many cached pubkeys are aggregated by k_pk_agg's wavefront
-// tree instead of serially on the set's k_prep lane.
+// Sets with at least this many cached pubkeys are aggregated by a tree (k_pk_agg16 on a
+// 16-lane team up to BGV_PK_TEAM_MAX keys, k_pk_agg on a whole wave above) instead of
+// serially on the set's k_prep lane.
 #ifndef BGV_PK_TREE_MIN
 #define BGV_PK_TREE_MIN 16
+#endif
+#ifndef BGV_PK_TEAM_MAX
+#define BGV_PK_TEAM_MAX 256
 #endif
 #define BGV_KATTR __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE, BGV_WPE)))
 #define BGV_KATTR_PREP __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_PREP, BGV_WPE_PREP)))

@@ -1,8 +1,9 @@
 // Per-set preparation kernels (gfx950): k_pk_agg and k_prep (see bgv_api.cpp for the
 // launch order of a verify call and bgv_k_miller.hip / bgv_k_final.hip for the rest).
 //
-//   k_pk_agg   (only when a call holds a set with >= BGV_PK_TREE_MIN cached keys) one
-//              wavefront per such set sums its keys with a ds_swizzle/ds_bpermute tree
+//   k_pk_agg16 / k_pk_agg  (only when a call holds a set with >= BGV_PK_TREE_MIN cached
+//              keys) a team of 16 lanes per committee-sized set, a whole wavefront per set
+//              above BGV_PK_TEAM_MAX keys, sums its keys with a ds_swizzle/ds_bpermute tree
 //   k_prep_a / k_prep_b   the latency path for small calls (bgv_latency_max): the same
 //              work over two launches with twice the lanes per set, so the longest chain
 //              per lane roughly halves: (a) one SSWU map + isogeny per lane for u0 and u1,
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   const uint32_t s = blockIdx.x;
   if (s >= nslots) return;
   const bgv_dslot& d = slots[s];
-  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < BGV_PK_TREE_MIN) return;
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk <= BGV_PK_TEAM_MAX) return;
   const uint32_t l = threadIdx.x;
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
@@ -323,6 +324,29 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
   }
 }
 
+// Committee-sized sets (BGV_PK_TREE_MIN..BGV_PK_TEAM_MAX cached keys, e.g. 128-key
+// attestation aggregates) on a team of 16 lanes, four sets per wave: lane l sums keys
+// l, l + 16, ... with mixed additions, then four ds_swizzle butterfly levels (xor 8..1, inside
+// the team).  A whole wave per 128-key set spent ~4x the lane work on the tree levels.
+__global__ void __launch_bounds__(64) k_pk_agg16(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                 const uint32_t* __restrict__ pk_idx,
+                                                 const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blockIdx.x * (64 / 16) + threadIdx.x / 16;
+  const uint32_t l = threadIdx.x % 16;
+  const bgv_dslot* d = s < nslots ? &slots[s] : nullptr;
+  const bool act = d && !(d->flags & BGV_SLOT_PAD) && (d->flags & BGV_SLOT_PK_CACHED) &&
+                   d->n_pk >= BGV_PK_TREE_MIN && d->n_pk <= BGV_PK_TEAM_MAX;
+  g1_jac acc = jac_infinity<fp_t>();
+  if (act)
+    for (uint32_t k = l; k < d->n_pk; k += 16) acc = jac_add_aff(acc, cache[pk_idx[d->pk_off + k]]);
+  // every lane of the wave reaches the exchanges
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (act && l == 0) pk_agg[s] = acc;
+}
+
 // The three independent per-set tasks in one launch (blockIdx.y = task), so one
 // batch keeps 3x the wavefronts in flight on a single stream.
 __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
@@ -366,6 +390,9 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   // k_pk_agg only when some set is large enough; otherwise k_prep sums serially (null pk_agg)
   const bool tree = b.max_npk >= BGV_PK_TREE_MIN;
   if (tree)
+    hipLaunchKernelGGL(k_pk_agg16, dim3(nblk(n, 4)), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
+                       reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
+  if (b.max_npk > BGV_PK_TEAM_MAX)
     hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
                        reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
   if (n + b.ngroups <= bgv_latency_max()) {
@@ -389,7 +416,8 @@ hipError_t bgv_launch_aggregate(const bgv_dslot* slot, const uint32_t* idx, uint
   const g1_aff* c = reinterpret_cast<const g1_aff*>(cache);
   g1_jac* a = reinterpret_cast<g1_jac*>(agg);
   const bool tree = n >= BGV_PK_TREE_MIN;
-  if (tree) hipLaunchKernelGGL(k_pk_agg, dim3(1), dim3(64), 0, st, slot, 1u, idx, c, a);
+  if (tree && n <= BGV_PK_TEAM_MAX) hipLaunchKernelGGL(k_pk_agg16, dim3(1), dim3(64), 0, st, slot, 1u, idx, c, a);
+  if (tree && n > BGV_PK_TEAM_MAX) hipLaunchKernelGGL(k_pk_agg, dim3(1), dim3(64), 0, st, slot, 1u, idx, c, a);
   hipLaunchKernelGGL(k_pk_sum_out, dim3(1), dim3(64), 0, st, slot, idx, c, tree ? a : nullptr, out96);
   return hipGetLastError();
 }

@@ -222,21 +222,26 @@ BGV_HD int bgv_opaque0() {
   return z;
 }
 
-// [k]P for a 64-bit (lane-varying) scalar: left-to-right, 2-bit fixed window
-// with a 3-entry table; the add is computed in every lane and selected, so a
-// wave never diverges on scalar bits.  The table lives in memory and one entry is
-// loaded per window (the accumulator and the addition's temporaries fill the registers).
+// [k]P for a 64-bit (lane-varying) scalar: left-to-right fixed window of BGV_MUL_WINDOW
+// bits over the table P, 2P, ..., (2^w - 1)P; the add is computed in every lane and
+// selected, so a wave never diverges on scalar bits.  The table lives in memory and one
+// entry is loaded per window (the accumulator and the addition's temporaries fill the
+// registers).
+#ifndef BGV_MUL_WINDOW
+#define BGV_MUL_WINDOW 3
+#endif
 template <class F>
 BGV_NOINLINE jac_t<F> jac_mul_u64(const jac_t<F>& p, uint64_t k) {
-  jac_t<F> tab[4];
+  constexpr int W = BGV_MUL_WINDOW, NT = 1 << W, NWIN = (64 + W - 1) / W;
+  jac_t<F> tab[NT];
   tab[1] = p;
   tab[2] = jac_dbl(p);
-  tab[3] = jac_add(tab[2], p);
+  BGV_NO_UNROLL for (int i = 3; i < NT; ++i) tab[i] = jac_add(tab[i - 1], p);
   tab[0] = tab[1];
   jac_t<F> acc = jac_infinity<F>();
-  BGV_NO_UNROLL for (int i = 62; i >= 0; i -= 2) {
-    acc = jac_dbl(jac_dbl(acc));
-    const uint32_t d = (uint32_t)(k >> i) & 3u;
+  BGV_NO_UNROLL for (int j = NWIN - 1; j >= 0; --j) {
+    BGV_UNROLL for (int t = 0; t < W; ++t) acc = jac_dbl(acc);
+    const uint32_t d = (uint32_t)(k >> (W * j)) & (uint32_t)(NT - 1);
     const jac_t<F> sum = jac_add(acc, tab[d]);
     acc = jac_select(d != 0u, acc, sum);
   }
