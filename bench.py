@@ -194,10 +194,10 @@ def aggregate_throughput(ctx, native, nkeys, calls=1024, inflight=128):
 
     assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
     done.clear()
-    ctx.set_batching(inflight * nsets, 20000)
+    ctx.set_batching(inflight * nsets, 20000, 20000)
     with ThreadPoolExecutor(max_workers=inflight) as pool:
         res = list(pool.map(call, range(calls)))
-    ctx.set_batching(131072, 2000)
+    ctx.set_batching(131072, 2000, 200)
     assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
     done.sort()
     a, b = 2 * inflight - 1, len(done) - 1
@@ -423,14 +423,14 @@ def main():
     bcalls = args.calls_per_batch or super_batch_calls(args.steps, args.nsets, ndisp)
     # the window opens on a super-batch boundary: at least `warmup` calls complete before it
     warm_calls = -(-args.warmup // bcalls) * bcalls
-    ctx.set_batching(bcalls * args.nsets, 200000)
+    ctx.set_batching(bcalls * args.nsets, 200000, 200000)
     ctx.profile(1)
     barrier()
     cuda_sync()
     win = stream_window(step, expect, warm_calls, args.steps, max(args.inflight, 3 * bcalls))
     cuda_sync()
     barrier()
-    ctx.set_batching(131072, 2000)
+    ctx.set_batching(131072, 2000, 200)
     elapsed = barrier.max(win["elapsed"])
     lat = win["latencies"]
     stats = win["stats"]

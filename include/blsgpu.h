@@ -196,10 +196,12 @@ int bgv_sign(bgv_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, size_t n, ui
 /* Super-batch geometry: verify calls queued within coalesce_us of each other are merged
  * into one device launch of at most max_batch_slots sets (the GPU form of the pool's
  * MAX_BUFFERED_SIGS / MAX_BUFFER_WAIT_MS and prepareWork packaging,
- * multithread/index.ts:39-57,386-401).  max_batch_slots = 0 and coalesce_us = UINT32_MAX
- * leave a value unchanged.  Defaults: 131072 sets, 2000 us (env BGV_MAX_BATCH_SLOTS,
- * BGV_COALESCE_US). */
-int bgv_set_batching(bgv_ctx* ctx, uint32_t max_batch_slots, uint32_t coalesce_us);
+ * multithread/index.ts:39-57,386-401).  While no super-batch is running the window is
+ * idle_coalesce_us instead (at most coalesce_us), so a lone call launches at once.
+ * max_batch_slots = 0 and a window of UINT32_MAX leave a value unchanged.  Defaults:
+ * 131072 sets, 2000 us, 200 us (env BGV_MAX_BATCH_SLOTS, BGV_COALESCE_US,
+ * BGV_IDLE_COALESCE_US). */
+int bgv_set_batching(bgv_ctx* ctx, uint32_t max_batch_slots, uint32_t coalesce_us, uint32_t idle_coalesce_us);
 
 /* Deterministic batch randomizers for tests (seed != 0: splitmix64 stream;
  * seed == 0: getrandom(), the default). */

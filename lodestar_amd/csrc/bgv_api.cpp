@@ -78,6 +78,14 @@ static size_t coalesce_us() {
   static const size_t v = env_size("BGV_COALESCE_US", BGV_COALESCE_US, 0);
   return v;
 }
+// the window while no super-batch is running: a lone call (block import, a quiet gossip
+// moment) then launches almost at once instead of waiting the full window for company
+// that is not coming (BGV_IDLE_COALESCE_US env)
+#define BGV_IDLE_COALESCE_US 200
+static size_t idle_coalesce_us() {
+  static const size_t v = env_size("BGV_IDLE_COALESCE_US", BGV_IDLE_COALESCE_US, 0);
+  return v;
+}
 static int dispatchers_per_device() {
   static const int v = (int)env_size("BGV_DISPATCHERS", BGV_DISPATCHERS, 1);
   return v;
@@ -284,6 +292,8 @@ struct bgv_ctx {
   // super-batch geometry (bgv_set_batching; env defaults at bgv_init)
   std::atomic<uint32_t> max_slots{BGV_MAX_BATCH_SLOTS};
   std::atomic<uint32_t> coalesce{BGV_COALESCE_US};
+  std::atomic<uint32_t> idle_coalesce{BGV_IDLE_COALESCE_US};
+  std::atomic<int> running{0};  // super-batches being run by dispatchers
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
   // dispatch
@@ -859,7 +869,10 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
         return n;
       };
       const size_t cap = c->max_slots.load();
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(c->coalesce.load());
+      // a full window only while another super-batch keeps the device busy anyway
+      const size_t win = c->running.load() > 0 ? c->coalesce.load()
+                                               : std::min<size_t>(c->coalesce.load(), c->idle_coalesce.load());
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(win);
       while (!c->stop && queued_slots() < cap &&
              c->qcv.wait_until(lk, until) != std::cv_status::timeout) {
       }
@@ -878,7 +891,9 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
     int rc;
     {
       std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+      c->running.fetch_add(1);
       rc = run_batch(c, *d, *x, calls);
+      c->running.fetch_sub(1);
     }
     for (Call* call : calls) {
       if (rc != BGV_OK)
@@ -920,6 +935,7 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   }
   c->max_slots = (uint32_t)max_batch_slots();
   c->coalesce = (uint32_t)coalesce_us();
+  c->idle_coalesce = (uint32_t)idle_coalesce_us();
   const int n = (devices && ndev > 0) ? ndev : 1;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
@@ -968,10 +984,11 @@ int bgv_destroy(bgv_ctx* c) {
   return BGV_OK;
 }
 
-int bgv_set_batching(bgv_ctx* c, uint32_t max_batch_slots, uint32_t coalesce_us) {
+int bgv_set_batching(bgv_ctx* c, uint32_t max_batch_slots, uint32_t coalesce_us, uint32_t idle_coalesce_us) {
   if (!c) return -BGV_E_ARG;
   if (max_batch_slots) c->max_slots = std::max<uint32_t>(max_batch_slots, BGV_WAVE);
   if (coalesce_us != UINT32_MAX) c->coalesce = coalesce_us;
+  if (idle_coalesce_us != UINT32_MAX) c->idle_coalesce = idle_coalesce_us;
   return BGV_OK;
 }
 

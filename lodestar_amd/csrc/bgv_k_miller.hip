@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
       pos += 2;
       const int rb = tmp_rec_bytes(T, M);
       int out;
-      const fp_t v = tmp_lane(Sm, prog + pos + c * rb, T, M, &out);
+      const fp_t v = tmp_lane_any(Sm, prog + pos + c * rb, T, M, &out);
       Sm[out] = v;  // no slot is read and written in one round (tools/gen_tmiller.py)
       __syncthreads();
       pos += BGV_TEAM * rb;

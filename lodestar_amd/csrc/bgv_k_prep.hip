@@ -35,7 +35,7 @@ struct tc_dev_engine {
       pos += 2;
       const int rb = tmp_rec_bytes(T, M);
       int out;
-      const fp_t v = tmp_lane(S, prog + pos + c * rb, T, M, &out);
+      const fp_t v = tmp_lane_any(S, prog + pos + c * rb, T, M, &out);
       S[out] = v;  // no slot is read and written in one round (tools/gen_tcurve.py)
       __syncthreads();
       pos += BGV_TEAM * rb;

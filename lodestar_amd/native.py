@@ -100,7 +100,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_keygen": ([P, P, SZ, ctypes.c_int64, P], ctypes.c_int),
             "bgv_sign": ([P, P, P, SZ, P], ctypes.c_int),
             "bgv_set_rng_seed": ([P, U64], ctypes.c_int),
-            "bgv_set_batching": ([P, U32, U32], ctypes.c_int),
+            "bgv_set_batching": ([P, U32, U32, U32], ctypes.c_int),
             "bgv_verify_partial": ([P, P, SZ, P, P], ctypes.c_int),
             "bgv_final_verify": ([P, P, SZ, P], ctypes.c_int),
             "bgv_strerror": ([ctypes.c_int], ctypes.c_char_p),
@@ -175,9 +175,10 @@ class Context:
         except Exception:
             pass
 
-    def set_batching(self, max_batch_slots: int = 0, coalesce_us: int = 0xFFFFFFFF):
+    def set_batching(self, max_batch_slots: int = 0, coalesce_us: int = 0xFFFFFFFF,
+                     idle_coalesce_us: int = 0xFFFFFFFF):
         """Super-batch geometry (bgv_set_batching); 0 / 0xFFFFFFFF leave a value unchanged."""
-        _check(self.lib.bgv_set_batching(self._h, max_batch_slots, coalesce_us))
+        _check(self.lib.bgv_set_batching(self._h, max_batch_slots, coalesce_us, idle_coalesce_us))
 
     def set_rng_seed(self, seed: int):
         _check(self.lib.bgv_set_rng_seed(self._h, seed))

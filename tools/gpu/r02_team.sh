@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r02 gpurun_out/lat
 export TMPDIR=/tmp
-TAG=${TAG:-t7}
+TAG=${TAG:-t9}
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r02/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/r02/pytest_$TAG.log; tail -4 gpurun_out/r02/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
