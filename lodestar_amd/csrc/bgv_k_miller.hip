@@ -21,8 +21,11 @@ extern "C" {
 // Lanes [0, nslots): f_i = MillerLoop(r pk, H(m)), 1 for slots that do not take part.
 // Lanes [nslots, nslots + ngroups): the group's signature pair MillerLoop(-G1, S_g) (1 for
 // an infinite S_g), so the group pairs run beside the set pairs instead of after them.
-__device__ __forceinline__ fp12_t group_pair(const g2_jac& S) {
-  return jac_is_inf(S) ? fp12_one() : miller_loop1(jac_from_aff(g1_neg_generator()), S);
+// -G1 in Jacobian form, in memory for miller_loop1m
+static __device__ const g1_jac kNegG1Jac = {{BGV_G1X}, {BGV_NEG_G1Y}, {BGV_ONE}};
+
+__device__ __forceinline__ fp12_t group_pair(const g2_jac* S) {
+  return jac_is_inf(*S) ? fp12_one() : miller_loop1m(&kNegG1Jac, S);
 }
 
 __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t nslots,
@@ -33,17 +36,17 @@ __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < nslots) {
     fp12_t r = fp12_one();
-    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1(rpk[s], h[s]);
+    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1m(rpk + s, h + s);
     f[s] = r;
   } else if (s - nslots < ngroups) {
-    gpair[s - nslots] = group_pair(gsum[s - nslots]);
+    gpair[s - nslots] = group_pair(gsum + (s - nslots));
   }
 }
 
 // retry rounds: the signature pairs of the round's parts alone
 __global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < ngroups) gpair[g] = group_pair(gsum[g]);
+  if (g < ngroups) gpair[g] = group_pair(gsum + g);
 }
 
 // S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an

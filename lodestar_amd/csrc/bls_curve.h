@@ -6,6 +6,7 @@
 // rare-case branches (equal inputs -> double, infinity operands).
 #pragma once
 #include "bls_field.h"
+#include "bls_lazy.h"
 
 // ---------------------------------------------------------------------------
 // overload set so the point code is written once for Fp and Fp2
@@ -93,43 +94,50 @@ BGV_HD jac_t<F> jac_neg(const jac_t<F>& p) {
 #define BGV_CURVE_ATTR BGV_HD
 #endif
 
-// dbl-2009-l
+// dbl-2009-l on lazy values (bls_lazy.h): E = 3A, F = E^2 = 9 A^2; the same field elements
+// as the eager formulas, each output reduced once (< 2p)
 template <class F>
 BGV_CURVE_ATTR jac_t<F> jac_dbl(const jac_t<F>& p) {
-  F A = f_sqr(p.x);
-  F B = f_sqr(p.y);
-  F C = f_sqr(B);
-  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
-  F E = f_add(f_dbl(A), A);
-  F Fq = f_sqr(E);
+  const auto X = L_in(p.x), Y = L_in(p.y), Z = L_in(p.z);
+  const auto A = L_sqr(X);
+  const auto B = L_sqr(Y);
+  const auto C = L_sqr(B);
+  const auto D = L_norm(L_dbl(L_sub(L_sqr(L_norm(L_add(X, B))), L_add(A, C))));
+  const auto X3 = L_norm(L_sub(L_mulk<9>(L_sqr(A)), L_dbl(D)));
+  const auto Y3 = L_sub(L_mulk<3>(L_mul(A, L_norm(L_sub(D, X3)))), L_mulk<8>(C));
   jac_t<F> r;
-  r.x = f_sub(Fq, f_dbl(D));
-  F C8 = f_dbl(f_dbl(f_dbl(C)));
-  r.y = f_sub(f_mul(E, f_sub(D, r.x)), C8);
-  r.z = f_dbl(f_mul(p.y, p.z));
+  r.x = L_out(X3);
+  r.y = L_out(Y3);
+  r.z = L_out(L_dbl(L_mul(Y, Z)));
   return r;
 }
 
-// add-2007-bl with the generic-case formulas; flags equal/opposite inputs.
+// add-2007-bl with the generic-case formulas (I = (2H)^2 = 4 HH, J = H I, V = U1 I);
+// flags equal/opposite inputs.
 template <class F>
 BGV_HD jac_t<F> jac_add_raw(const jac_t<F>& p, const jac_t<F>& q, bool* h_zero, bool* r_zero) {
-  F Z1Z1 = f_sqr(p.z);
-  F Z2Z2 = f_sqr(q.z);
-  F U1 = f_mul(p.x, Z2Z2);
-  F U2 = f_mul(q.x, Z1Z1);
-  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
-  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
-  F H = f_sub(U2, U1);
-  F I = f_sqr(f_dbl(H));
-  F J = f_mul(H, I);
-  F rr = f_dbl(f_sub(S2, S1));
-  F V = f_mul(U1, I);
+  const auto X1 = L_in(p.x), Y1 = L_in(p.y), Z1 = L_in(p.z);
+  const auto X2 = L_in(q.x), Y2 = L_in(q.y), Z2 = L_in(q.z);
+  const auto Z1Z1 = L_sqr(Z1);
+  const auto Z2Z2 = L_sqr(Z2);
+  const auto U1 = L_mul(X1, Z2Z2);
+  const auto U2 = L_mul(X2, Z1Z1);
+  const auto S1 = L_mul(L_mul(Y1, Z2), Z2Z2);
+  const auto S2 = L_mul(L_mul(Y2, Z1), Z1Z1);
+  const auto H = L_norm(L_sub(U2, U1));
+  const auto HH = L_sqr(H);
+  const auto J = L_mulk<4>(L_mul(H, HH));
+  const auto rr = L_red(L_dbl(L_sub(S2, S1)));
+  const auto V = L_mulk<4>(L_mul(U1, HH));
+  const auto X3 = L_norm(L_sub(L_sqr(rr), L_add(J, L_dbl(V))));
+  const auto Y3 = L_sub(L_mul(rr, L_norm(L_sub(V, X3))), L_dbl(L_mul(S1, L_norm(J))));
+  const auto Z3 = L_mul(L_sub(L_sqr(L_norm(L_add(Z1, Z2))), L_add(Z1Z1, Z2Z2)), H);
   jac_t<F> r;
-  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(S1, J)));
-  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
-  *h_zero = f_is_zero(H);
-  *r_zero = f_is_zero(rr);
+  r.x = L_out(X3);
+  r.y = L_out(Y3);
+  r.z = L_out(Z3);
+  *h_zero = L_is_zero(H);
+  *r_zero = L_is_zero(rr);
   return r;
 }
 
@@ -145,24 +153,28 @@ BGV_CURVE_ATTR jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
   return r;
 }
 
-// madd-2007-bl: p Jacobian + q affine (q never infinity)
+// madd-2007-bl: p Jacobian + q affine (q never infinity), lazy values as in jac_add_raw
 template <class F>
 BGV_HD jac_t<F> jac_add_aff_raw(const jac_t<F>& p, const aff_t<F>& q, bool* h_zero, bool* r_zero) {
-  F Z1Z1 = f_sqr(p.z);
-  F U2 = f_mul(q.x, Z1Z1);
-  F S2 = f_mul(q.y, f_mul(p.z, Z1Z1));
-  F H = f_sub(U2, p.x);
-  F HH = f_sqr(H);
-  F I = f_dbl(f_dbl(HH));
-  F J = f_mul(H, I);
-  F rr = f_dbl(f_sub(S2, p.y));
-  F V = f_mul(p.x, I);
+  const auto X1 = L_in(p.x), Y1 = L_in(p.y), Z1 = L_in(p.z);
+  const auto X2 = L_in(q.x), Y2 = L_in(q.y);
+  const auto Z1Z1 = L_sqr(Z1);
+  const auto U2 = L_mul(X2, Z1Z1);
+  const auto S2 = L_mul(Y2, L_mul(Z1, Z1Z1));
+  const auto H = L_norm(L_sub(U2, X1));
+  const auto HH = L_sqr(H);
+  const auto J = L_mulk<4>(L_mul(H, HH));
+  const auto rr = L_red(L_dbl(L_sub(S2, Y1)));
+  const auto V = L_mulk<4>(L_mul(X1, HH));
+  const auto X3 = L_norm(L_sub(L_sqr(rr), L_add(J, L_dbl(V))));
+  const auto Y3 = L_sub(L_mul(rr, L_norm(L_sub(V, X3))), L_dbl(L_mul(Y1, L_norm(J))));
+  const auto Z3 = L_sub(L_sqr(L_norm(L_add(Z1, H))), L_add(Z1Z1, HH));
   jac_t<F> r;
-  r.x = f_sub(f_sub(f_sqr(rr), J), f_dbl(V));
-  r.y = f_sub(f_mul(rr, f_sub(V, r.x)), f_dbl(f_mul(p.y, J)));
-  r.z = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
-  *h_zero = f_is_zero(H);
-  *r_zero = f_is_zero(rr);
+  r.x = L_out(X3);
+  r.y = L_out(Y3);
+  r.z = L_out(Z3);
+  *h_zero = L_is_zero(H);
+  *r_zero = L_is_zero(rr);
   return r;
 }
 

@@ -4,6 +4,7 @@
 // pairing, which has the same kernel since gcd(3, r) = 1).
 #pragma once
 #include "bls_curve.h"
+#include "bls_lazy.h"
 
 // The G1 point of a Miller loop in Jacobian form P = (X : Y : Z) (no inversion after
 // r_i * pk_i): every line is scaled by Z^3, an Fp factor the final exponentiation kills,
@@ -146,10 +147,111 @@ BGV_HD fp12_t fp12_from_line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) 
   return fp12_t{fp6_t{l0, l1, fp2_zero()}, fp6_t{fp2_zero(), l3, fp2_zero()}};
 }
 
+// ---------------------------------------------------------------------------
+// The same Miller loop on lazy values (bls_lazy.h): the line formulas and the Fp12
+// steps compute the same field elements as miller_dbl / miller_add_jq /
+// fp12_sqr / fp12_mul_line, with the additions and subtractions left unreduced and the
+// bounds checked at compile time.  T and f are brought back to < 2p once per step.
+// ---------------------------------------------------------------------------
+struct lz_tpt {
+  lz2r x, y, z;
+};
+typedef lz12<LMASK, 2> lzf12;
+
+struct lz_mp {
+  lzr xn, yp, zp3;
+};
+struct lz_jq {
+  lz2r qx, qy, qz, zz, xz, y2z, zzz_xn, zzz_yp;
+};
+
+// doubling step: lines of miller_dbl (E = 3A, F = E^2 = 9 A^2, E X = 3 A X)
+BGV_MILLER_ATTR void lz_miller_dbl_lines(lz_tpt& t, const lz_mp& P, lz2r* l0, lz2r* l1, lz2r* l3) {
+  const lz2r A = lz2_sqr(t.x);
+  const lz2r B = lz2_sqr(t.y);
+  const lz2r C = lz2_sqr(B);
+  const lz2r ZZ = lz2_sqr(t.z);
+  const auto D = lz2_norm(lz2_dbl(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.x, B))), lz2_add(A, C))));
+  *l0 = lz2_mul_fp(lz2_sub(lz2_mulk<3>(lz2_mul(A, t.x)), lz2_dbl(B)), P.zp3);
+  *l1 = lz2_mul_fp(lz2_mulk<3>(lz2_mul(A, ZZ)), P.xn);
+  const auto X3 = lz2_sub(lz2_mulk<9>(lz2_sqr(A)), lz2_dbl(D));
+  const auto Y3 = lz2_sub(lz2_mulk<3>(lz2_mul(A, lz2_norm(lz2_sub(D, X3)))), lz2_mulk<8>(C));
+  const auto Z3 = lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.y, t.z))), lz2_add(B, ZZ));
+  *l3 = lz2_mul_fp(lz2_mul(Z3, ZZ), P.yp);
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+}
+
+BGV_MILLER_ATTR lzf12 lz_miller_dbl_first(lz_tpt& t, const lz_mp& P) {
+  lz2r l0, l1, l3;
+  lz_miller_dbl_lines(t, P, &l0, &l1, &l3);
+  const lz2r z = lz2r{lz_in(fp_zero()), lz_in(fp_zero())};
+  return lzf12{lz6<LMASK, 2>{l0, l1, z}, lz6<LMASK, 2>{z, l3, z}};
+}
+
+BGV_MILLER_ATTR lzf12 lz_miller_dbl_step(const lzf12& f, lz_tpt& t, const lz_mp& P) {
+  lz2r l0, l1, l3;
+  lz_miller_dbl_lines(t, P, &l0, &l1, &l3);
+  return lz12_red(lz12_mul_line(lz12_red(lz12_sqr(f)), l0, l1, l3));
+}
+
+// addition step with the Jacobian-Q constants (miller_add_jq; J = 4 H HH, V = 4 U1 HH)
+BGV_MILLER_ATTR lzf12 lz_miller_add_step(const lzf12& f, lz_tpt& t, const lz_jq& c) {
+  const lz2r ZZ = lz2_sqr(t.z);
+  const auto U1 = lz2_mul(t.x, c.zz);
+  const auto U2 = lz2_mul(c.qx, ZZ);
+  const auto S1 = lz2_mul(t.y, lz2_mul(c.zz, c.qz));
+  const auto S2 = lz2_mul(c.qy, lz2_mul(t.z, ZZ));
+  const auto H = lz2_norm(lz2_sub(U2, U1));
+  const lz2r HH = lz2_sqr(H);
+  const auto J = lz2_mulk<4>(lz2_mul(H, HH));
+  const lz2r r = lz2_red(lz2_dbl(lz2_sub(S2, S1)));
+  const auto V = lz2_mulk<4>(lz2_mul(U1, HH));
+  const auto X3 = lz2_norm(lz2_sub(lz2_sqr(r), lz2_add(J, lz2_dbl(V))));
+  const auto Y3 = lz2_sub(lz2_mul(r, lz2_norm(lz2_sub(V, X3))), lz2_dbl(lz2_mul(S1, lz2_norm(J))));
+  const auto Z3 = lz2_mul(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, c.qz))), lz2_add(ZZ, c.zz)), H);
+  const auto l0 = lz2_norm(lz2_sub(lz2_mul(r, c.xz), lz2_mul(c.y2z, Z3)));
+  const lz2r l1 = lz2_red(lz2_mul(r, c.zzz_xn));
+  const lz2r l3 = lz2_red(lz2_mul(Z3, c.zzz_yp));
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+  return lz12_red(lz12_mul_line(f, l0, l1, l3));
+}
+
 // f_{|x|,Q}(P) for ONE pair (conjugated for x < 0): P and Q Jacobian (Z != 0).
 // The per-set Miller loop of the blst batch equation (maybeBatch.ts:18-25 ->
 // verifyMultipleAggregateSignatures): e(r_i pk_i, H(m_i)); the signature side
 // e(-G1, sum r_i sig_i) is one team loop per device group (bls_team.h).
+#ifndef BGV_MILLER_EAGER
+// P and Q are read from memory: the Jacobian-Q constants of the 5 addition steps (16 Fp,
+// 224 VGPRs) are recomputed there from Q and P (~19 products per step) instead of staying
+// live across the 63 doubling steps, where the registers hold f, T and the step's
+// temporaries.  The opaque index keeps the compiler from hoisting the loads.
+BGV_MILLER_LOOP_ATTR fp12_t miller_loop1m(const g1_jac* pm, const g2_jac* qm) {
+  const lz_mp P = [&] {
+    const miller_p P0 = miller_p_make(pm[0]);
+    return lz_mp{lz_in(P0.xn), lz_in(P0.yp), lz_in(P0.zp3)};
+  }();
+  lz_tpt t = {lz2_in(qm[0].x), lz2_in(qm[0].y), lz2_in(qm[0].z)};
+  const uint64_t X = BGV_X_ABS;
+  lzf12 f = lz_miller_dbl_first(t, P);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if ((X >> (i + 1)) & 1) {
+      const int o = bgv_opaque0();
+      const miller_p P0 = miller_p_make(pm[o]);
+      const miller_jq c0 = miller_jq_make(qm[o], P0);
+      const lz_jq c = {lz2_in(c0.q.x), lz2_in(c0.q.y), lz2_in(c0.q.z),      lz2_in(c0.zz),
+                       lz2_in(c0.xz),  lz2_in(c0.y2z), lz2_in(c0.zzz_xn), lz2_in(c0.zzz_yp)};
+      f = lz_miller_add_step(f, t, c);
+    }
+    f = lz_miller_dbl_step(f, t, P);
+  }
+  return fp12_conj(lz12_out(f));
+}
+BGV_HD fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) { return miller_loop1m(&p, &q); }
+#else
 BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) {
   const miller_p P = miller_p_make(p);
 #ifndef BGV_MILLER_JQ_RECOMPUTE
@@ -176,6 +278,7 @@ BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) {
   }
   return fp12_conj(f);
 }
+#endif
 
 // a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
 BGV_NOINLINE fp12_t cyclotomic_pow_x(const fp12_t& a) {

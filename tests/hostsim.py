@@ -14,7 +14,8 @@ def build(force=False):
     deps = [SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in deps):
         return LIB
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", LIB, SRC])
+    # -DBGV_LAZY_CHECK: every lazy value (bls_lazy.h) is checked against its static bounds
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-DBGV_LAZY_CHECK", "-shared", "-fPIC", "-o", LIB, SRC])
     return LIB
 
 
