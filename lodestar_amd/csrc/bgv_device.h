@@ -15,10 +15,11 @@
 #ifndef BGV_WPE
 #define BGV_WPE 1
 #endif
-// k_prep runs 3 x nslots lanes of shorter tasks: two waves per SIMD measured faster
-// (36.6 vs 45.3 ms per 131072 slots), the long-chain kernels stay at one.
+// k_prep: one wave per SIMD since the lazy point formulas (bls_lazy.h): 15.0 vs 16.1 ms per
+// 64,512-set call (profiles/r02s3/roof_p1_*.json); two waves per SIMD were faster (36.6 vs
+// 45.3 ms per 131,072 slots) with the eager formulas.  k_miller at two waves: 22.3 vs 11.7 ms.
 #ifndef BGV_WPE_PREP
-#define BGV_WPE_PREP 2
+#define BGV_WPE_PREP 1
 #endif
 // Sets with at least this many cached pubkeys are aggregated by a tree (k_pk_agg16 on a
 // 16-lane team up to BGV_PK_TEAM_MAX keys, k_pk_agg on a whole wave above) instead of

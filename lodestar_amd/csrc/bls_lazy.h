@@ -227,28 +227,29 @@ BGV_HD lz<LMASK, VA> lz_norm(const lz<LA, VA>& a) {
   return r;
 }
 
-// back to the fp_t invariant: normalize, then subtract q p, q = top / (P13 + 1).
-// q p <= top 2^364 <= value, and value - q p < (P13 + 1 + q) 2^364 + (value mod 2^364) < 2p.
+// back to the fp_t invariant in one signed carry chain: subtract q p with q = top / (P13 + 1)
+// taken from the unnormalized top limb.  q p <= top 2^364 <= value (the lower limbs are
+// non-negative), and value - q p < (P13 + 1 + q) 2^364 + sum_{i<13} a_i 2^(28 i)
+// < p + (q + 1) 2^364 + 2^368 < 2p for any q < 2^16; the chain leaves limbs < 2^28.
 template <uint64_t LA, uint64_t VA>
 BGV_HD fp_t lz_out(const lz<LA, VA>& a) {
   fp_t r;
   if constexpr (LA <= LMASK && VA <= 2) {
     BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i];
-  } else {
+  } else if constexpr (VA <= 2) {
     const lz<LMASK, VA> n = lz_norm(a);
-    if constexpr (VA <= 2) {
-      BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = n.v[i];
-    } else {
-      const uint32_t P_[NL] = BGV_P_LIMBS;
-      const uint32_t q = n.v[NL - 1] / (uint32_t)(lzc::P13 + 1);
-      int64_t c = 0;
-      BGV_UNROLL for (int i = 0; i < NL - 1; ++i) {
-        const int64_t s = (int64_t)n.v[i] - (int64_t)((uint64_t)q * P_[i]) + c;
-        r.v[i] = (uint32_t)s & LMASK;
-        c = s >> LBITS;
-      }
-      r.v[NL - 1] = (uint32_t)((int64_t)n.v[NL - 1] - (int64_t)q * P_[NL - 1] + c);
+    BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = n.v[i];
+  } else {
+    static_assert(LA / (lzc::P13 + 1) < (1ull << 16), "lz_out: quotient estimate too large");
+    const uint32_t P_[NL] = BGV_P_LIMBS;
+    const uint32_t q = a.v[NL - 1] / (uint32_t)(lzc::P13 + 1);
+    int64_t c = 0;
+    BGV_UNROLL for (int i = 0; i < NL - 1; ++i) {
+      const int64_t s = (int64_t)a.v[i] - (int64_t)((uint64_t)q * P_[i]) + c;
+      r.v[i] = (uint32_t)s & LMASK;
+      c = s >> LBITS;
     }
+    r.v[NL - 1] = (uint32_t)((int64_t)a.v[NL - 1] - (int64_t)((uint64_t)q * P_[NL - 1]) + c);
   }
   LZ_CHECK(lz_in(r), "out");
   return r;
