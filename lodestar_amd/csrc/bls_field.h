@@ -308,58 +308,100 @@ BGV_HD fp_t fp_from_mont(const fp_t& a) {
   return fp_canon(fp_mul(a, one));
 }
 
-// a^e for a fixed (lane-uniform) exponent given as 32-bit little-endian words:
-// left-to-right sliding window of width 5 over a table of the 16 odd powers
-// a, a^3, ..., a^31.  The exponents used here have ~229 one bits in 381: the
-// window cuts the products from ~229 to ~84 (16 of them for the table).  All
-// control flow follows the exponent, so a wave never diverges.
-BGV_HD uint32_t exp_bit(const uint32_t* e, int i) { return (e[i >> 5] >> (i & 31)) & 1u; }
-
-BGV_NOINLINE fp_t fp_pow_words(const fp_t& a, const uint32_t* e, int nbits) {
-  fp_t tab[16];
-  tab[0] = a;
-  const fp_t a2 = fp_sqr(a);
-  BGV_NO_UNROLL for (int k = 1; k < 16; ++k) tab[k] = fp_mul(tab[k - 1], a2);
-  fp_t r = a;
+// a^e for a fixed exponent: left-to-right sliding window of width 5 over a table of the 16
+// odd powers a, a^3, ..., a^31.  The exponents used here have ~229 one bits in 381: the
+// window cuts the products from ~229 to ~84 (16 of them for the table).  The window
+// schedule is computed at compile time (bgv_make_sched) and read from constant memory with
+// scalar loads, so the loop does no per-bit exponent reads (these were scratch loads with a
+// wait each), and each window's table entry is loaded before its squarings.
+struct bgv_exp12 {
+  uint32_t w[12];
+};
+struct bgv_pow_sched {
+  int n;                // steps after the first window
+  int first;            // r starts as tab[first] = a^(2 first + 1)
+  uint32_t step[112];   // step k: (step & 0xff) squarings, then a product by tab[step >> 8]
+                        // (0xff: none -- trailing squarings); dwords for scalar loads
+};
+constexpr int bgv_exp_bit(const bgv_exp12& e, int i) { return (int)((e.w[i >> 5] >> (i & 31)) & 1u); }
+constexpr bgv_pow_sched bgv_make_sched(bgv_exp12 e, int nbits) {
+  bgv_pow_sched s{};
   bool started = false;
+  int pending = 0;
   int i = nbits - 1;
-  BGV_NO_UNROLL while (i >= 0) {
-    if (!exp_bit(e, i)) {
-      r = fp_sqr(r);  // only reached once started: the top bit is 1
+  while (i >= 0) {
+    if (!bgv_exp_bit(e, i)) {
+      ++pending;
       --i;
       continue;
     }
     int j = i - 4 > 0 ? i - 4 : 0;
-    while (!exp_bit(e, j)) ++j;
-    uint32_t w = 0;
-    for (int q = i; q >= j; --q) w = (w << 1) | exp_bit(e, q);
+    while (!bgv_exp_bit(e, j)) ++j;
+    int w = 0;
+    for (int q = i; q >= j; --q) w = (w << 1) | bgv_exp_bit(e, q);
     if (started) {
-      BGV_NO_UNROLL for (int q = i; q >= j; --q) r = fp_sqr(r);
-      r = fp_mul(r, tab[w >> 1]);
+      s.step[s.n] = (uint32_t)(pending + (i - j + 1)) | ((uint32_t)(w >> 1) << 8);
+      ++s.n;
     } else {
-      r = tab[w >> 1];
+      s.first = w >> 1;
       started = true;
     }
+    pending = 0;
     i = j - 1;
+  }
+  if (pending) {
+    s.step[s.n] = (uint32_t)pending | (0xffu << 8);
+    ++s.n;
+  }
+  return s;
+}
+#if defined(__HIPCC__)
+#define BGV_CONSTANT __constant__
+#else
+#define BGV_CONSTANT
+#endif
+enum { BGV_POW_INV = 0, BGV_POW_P34 = 1, BGV_POW_SQRT = 2 };
+static BGV_CONSTANT const bgv_pow_sched kBgvPow[3] = {
+    bgv_make_sched(bgv_exp12{BGV_EXP_P_MINUS_2}, 381),
+    bgv_make_sched(bgv_exp12{BGV_EXP_P_MINUS_3_DIV_4}, 379),
+    bgv_make_sched(bgv_exp12{BGV_EXP_P_PLUS_1_DIV_4}, 379),
+};
+
+template <int W>
+BGV_NOINLINE fp_t fp_pow_fixed(const fp_t& a) {
+  const bgv_pow_sched& s = kBgvPow[W];
+  fp_t tab[16];
+  fp_t cur = a;
+  tab[0] = a;
+  const fp_t a2 = fp_sqr(a);
+  BGV_NO_UNROLL for (int k = 1; k < 16; ++k) {
+    cur = fp_mul(cur, a2);
+    tab[k] = cur;
+  }
+  fp_t r = tab[s.first];
+  BGV_NO_UNROLL for (int k = 0; k < s.n; ++k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int ku = __builtin_amdgcn_readfirstlane(k);  // uniform: scalar loads of the schedule
+#else
+    const int ku = k;
+#endif
+    const uint32_t st = s.step[ku];
+    const int d = (int)(st >> 8), nsq = (int)(st & 0xff);
+    const fp_t m = tab[d & 15];
+    BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) r = fp_sqr(r);
+    if (d != 0xff) r = fp_mul(r, m);
   }
   return r;
 }
 
-BGV_HD fp_t fp_inv(const fp_t& a) {
-  const uint32_t e[12] = BGV_EXP_P_MINUS_2;
-  return fp_pow_words(a, e, 381);
-}
+BGV_HD fp_t fp_inv(const fp_t& a) { return fp_pow_fixed<BGV_POW_INV>(a); }
 
 // a^((p-3)/4): for a QR, a * t = sqrt(a) and t = 1/sqrt(a).
-BGV_HD fp_t fp_pow_p_minus_3_div_4(const fp_t& a) {
-  const uint32_t e[12] = BGV_EXP_P_MINUS_3_DIV_4;
-  return fp_pow_words(a, e, 379);
-}
+BGV_HD fp_t fp_pow_p_minus_3_div_4(const fp_t& a) { return fp_pow_fixed<BGV_POW_P34>(a); }
 
 // sqrt candidate; returns true iff a is a square (then *out = a^((p+1)/4)).
 BGV_HD bool fp_sqrt(fp_t* out, const fp_t& a) {
-  const uint32_t e[12] = BGV_EXP_P_PLUS_1_DIV_4;
-  fp_t s = fp_pow_words(a, e, 379);
+  fp_t s = fp_pow_fixed<BGV_POW_SQRT>(a);
   *out = s;
   return fp_eq(fp_sqr(s), a);
 }
