@@ -342,6 +342,8 @@ def stream_window(step, expect, warmup, steps, inflight):
             "calls_total": len(done)}
 
 
+# PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
+TRAFFIC_FILE = os.path.join("profiles", "r02s3", "traffic.json")
 ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
 
 
@@ -467,10 +469,10 @@ def main():
         work = {"k_miller": roof["sets"] * opc["k_miller"] + ngr * opc["k_final[group sig pair]"],
                 "k_prep": roof["sets"] * per_set["k_prep"]}[dom]
         achieved = work * MACS_PER_FP_MUL / (rk[dom] * 1e-3)
-        # HBM bytes of that same launch from the committed PMC passes (profiles/r02/traffic.json:
+        # HBM bytes of that same launch from the committed PMC passes (TRAFFIC_FILE:
         # (FETCH_SIZE x 2 + WRITE_SIZE) x 1024, rocprofv3 reports KB) and the algorithmic bytes
         traffic = hbm_gbs = None
-        tf = os.path.join(ROOT, "profiles", "r02", "traffic.json")
+        tf = os.path.join(ROOT, TRAFFIC_FILE)
         if os.path.exists(tf):
             rec = json.load(open(tf)).get(dom, {})
             if rec.get("sets") == roof["sets"]:
