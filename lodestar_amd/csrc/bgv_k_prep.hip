@@ -328,17 +328,33 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
 // attestation aggregates) on a team of 16 lanes, four sets per wave: lane l sums keys
 // l, l + 16, ... with mixed additions, then four ds_swizzle butterfly levels (xor 8..1, inside
 // the team).  A whole wave per 128-key set spent ~4x the lane work on the tree levels.
-__global__ void __launch_bounds__(64) k_pk_agg16(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                                 const uint32_t* __restrict__ pk_idx,
-                                                 const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
+// The lane's first key starts the sum (no addition to infinity), and each key is gathered
+// one addition ahead of its use.  A gather-latency-bound kernel: BGV_WPE_AGG waves per SIMD.
+#ifndef BGV_WPE_AGG
+#define BGV_WPE_AGG 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_AGG, BGV_WPE_AGG)))
+k_pk_agg16(const bgv_dslot* __restrict__ slots, uint32_t nslots, const uint32_t* __restrict__ pk_idx,
+           const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * (64 / 16) + threadIdx.x / 16;
   const uint32_t l = threadIdx.x % 16;
   const bgv_dslot* d = s < nslots ? &slots[s] : nullptr;
   const bool act = d && !(d->flags & BGV_SLOT_PAD) && (d->flags & BGV_SLOT_PK_CACHED) &&
                    d->n_pk >= BGV_PK_TREE_MIN && d->n_pk <= BGV_PK_TEAM_MAX;
   g1_jac acc = jac_infinity<fp_t>();
-  if (act)
-    for (uint32_t k = l; k < d->n_pk; k += 16) acc = jac_add_aff(acc, cache[pk_idx[d->pk_off + k]]);
+  if (act) {  // n_pk >= 16: every lane has a first key
+    const uint32_t* idx = pk_idx + d->pk_off;
+    const uint32_t n = d->n_pk;
+    acc = jac_from_aff(cache[idx[l]]);
+    uint32_t k = l + 16;
+    g1_aff cur = cache[idx[k < n ? k : l]];
+    for (; k < n; k += 16) {
+      const uint32_t kn = k + 16 < n ? k + 16 : k;
+      const g1_aff nxt = cache[idx[kn]];
+      acc = jac_add_aff(acc, cur);
+      cur = nxt;
+    }
+  }
   // every lane of the wave reaches the exchanges
   acc = jac_add(acc, point_xor<8>(acc));
   acc = jac_add(acc, point_xor<4>(acc));
