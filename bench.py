@@ -161,13 +161,15 @@ def block_import_latency(ctx, native, nkeys, runs=100):
             "runs": runs}
 
 
-def aggregate_throughput(ctx, native, nkeys, calls=1024, inflight=128):
+def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
     """config 2: 1024 aggregate sets x 128 distinct cached keys (contiguous committees),
     distinct signing roots, all valid, sent as the pool sends them (8 batchable jobs of
     128 sets, index.ts:155-166); `calls` such calls streaming with `inflight` outstanding.
-    Super-batches hold `inflight` calls (131,072 sets), so completions arrive in bursts of
-    `inflight`: the rate is taken between the end of the 2nd burst and the end of the last
-    (steady state, no pipeline fill or drain inside the window)."""
+    Super-batches hold `inflight` calls, so completions arrive in bursts of `inflight`: the
+    rate is taken between the end of the 2nd burst and the end of the last (steady state, no
+    pipeline fill or drain inside the window).  126 calls = 129,024 sets + 2,016 group pairs
+    = 131,040 k_miller lanes, two whole rounds of one wave per SIMD (128 calls would need a
+    third, 2 %-full round: 1.51 vs 1.62 M sets/s, profiles/r02s3/agg_inflight/)."""
     from concurrent.futures import ThreadPoolExecutor
     nsets, per = 1024, 128
     assert nsets * per <= nkeys

@@ -173,7 +173,9 @@ def test_config5_aggregate_variant_2048x512(big):
 
 def test_config5_shard_of_epoch_sweep(big):
     """Rank 0's 131,072 of 1,048,576 sets over the full 2^20-key cache (indices spread
-    over all of it), 1 % corrupted; verdicts by construction."""
+    over all of it), 1 % corrupted; verdicts by construction.  One super-batch of 131,072
+    slots: its 2,048 group pairs run on k_miller_team beside two full k_miller rounds
+    (bgv_launch_miller's round split)."""
     from lodestar_amd import native
     c, sks = big
     sets, expect = _gossip(c, sks, 1 << 17, 12345, 0x5)
