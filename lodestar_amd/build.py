@@ -38,8 +38,9 @@ def _headers():
     return out + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
 
 
-def build(force=False, verbose=True, lib=LIB, defines=()):
-    """defines: extra -D flags (tuning variants built to another `lib` path).  Objects are
+def build(force=False, verbose=True, lib=LIB, defines=(), extra_flags=()):
+    """defines: extra -D flags, extra_flags: extra compiler flags (tuning variants built to
+    another `lib` path).  Objects are
     cached per source under build/obj (the kernel unit takes minutes; the host unit seconds)
     and rebuilt when the source or any header is newer."""
     if not force and up_to_date(lib):
@@ -47,14 +48,16 @@ def build(force=False, verbose=True, lib=LIB, defines=()):
     os.makedirs(OBJ_DIR, exist_ok=True)
     hdr_mtime = max(os.path.getmtime(h) for h in _headers())
     objs, procs = [], []
-    tag = os.path.basename(lib) + ("." + "_".join(defines) if defines else "")
+    extra_flags = list(extra_flags)
+    tag = os.path.basename(lib) + ("." + "_".join(defines) if defines else "") + \
+        ("." + str(abs(hash(" ".join(extra_flags)))) if extra_flags else "")
     for src in SOURCES:
         obj = os.path.join(OBJ_DIR, tag + "." + os.path.basename(src) + ".o")
         fresh = (not force and os.path.exists(obj)
                  and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime))
         if not fresh:
             cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-                   "-c", src, "-o", obj + ".tmp"] + ["-D" + d for d in defines]
+                   "-c", src, "-o", obj + ".tmp"] + ["-D" + d for d in defines] + extra_flags
             if verbose:
                 print(" ".join(cmd), flush=True)
             procs.append((subprocess.Popen(cmd), obj))
@@ -98,9 +101,10 @@ def build_node(force=False, verbose=True):
 
 if __name__ == "__main__":
     if "--variant" in sys.argv:  # --variant NAME DEF1 [DEF2 ...]: lodestar_amd/libblsgpu_NAME.so
-        i = sys.argv.index("--variant")
+        i = sys.argv.index("--variant")    # (BGV_VARIANT_FLAGS env: extra compiler flags)
         name, defs = sys.argv[i + 1], sys.argv[i + 2:]
-        print(build(force=True, lib=os.path.join(HERE, "libblsgpu_%s.so" % name), defines=defs))
+        flags = os.environ.get("BGV_VARIANT_FLAGS", "").split()
+        print(build(force=True, lib=os.path.join(HERE, "libblsgpu_%s.so" % name), defines=defs, extra_flags=flags))
         sys.exit(0)
     build(force="--force" in sys.argv)
     build_node(force="--force" in sys.argv)
