@@ -55,6 +55,8 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on this device
+    local = int(os.environ.get("BGV_BENCH_DEVICE", local))
     return rank, world, local
 
 
