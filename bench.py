@@ -209,7 +209,10 @@ def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
     return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls "
                       "streaming, %d in flight; rate between the 2nd and the last super-batch completion"
                       % (calls, inflight),
-            "value": rate, "unit": "sets/s", "pubkeys_per_s": rate * per}
+            "value": rate, "unit": "sets/s", "pubkeys_per_s": rate * per,
+            # HBM bytes of the pubkey gather: one 112-B cache entry (affine G1,
+            # 28-bit Montgomery limbs) + one 4-B index per aggregated key
+            "pubkey_gather_GBps": rate * per * (112 + 4) / 1e9}
 
 
 def host_cpu():
