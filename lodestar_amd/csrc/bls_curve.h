@@ -87,12 +87,8 @@ BGV_HD jac_t<F> jac_neg(const jac_t<F>& p) {
 // Jacobian doubling/addition are inlined into their callers: the scalar-multiplication
 // loops ([x]P for the G2 subgroup check and cofactor clearing, r * pk) keep the point in
 // VGPRs instead of passing it through scratch on every step (k_prep 31.0 -> 29.4 ms per
-// 131,072 sets, tools/gpu/variants.sh).  -DBGV_CURVE_OUTLINE restores the calls.
-#ifdef BGV_CURVE_OUTLINE
-#define BGV_CURVE_ATTR BGV_NOINLINE
-#else
+// 131,072 sets with the eager formulas).
 #define BGV_CURVE_ATTR BGV_HD
-#endif
 
 // dbl-2009-l on lazy values (bls_lazy.h): E = 3A, F = E^2 = 9 A^2; the same field elements
 // as the eager formulas, each output reduced once (< 2p)

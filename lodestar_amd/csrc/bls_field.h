@@ -45,16 +45,11 @@
 #endif
 
 // The tower functions of the Miller-loop step (fp6_mul, fp6_mul_01, fp12_sqr, the
-// line products, miller_dbl/add) are inlined into miller_loop1, so f, T and the
+// line products, miller_dbl/add) are inlined into their callers, so f, T and the
 // lines stay in VGPRs and only fp_mul/fp_sqr are calls: out of line, every
 // by-reference argument and struct return went through scratch, and at one wave
-// per SIMD nothing hid that latency (k_miller 51.4 -> 41.3 ms per 131,072 sets,
-// tools/gpu/variants.sh).  -DBGV_MILLER_OUTLINE restores the calls.
-#ifdef BGV_MILLER_OUTLINE
-#define BGV_MILLER_ATTR BGV_NOINLINE
-#else
+// per SIMD nothing hid that latency (k_miller 51.4 -> 41.3 ms per 131,072 sets).
 #define BGV_MILLER_ATTR BGV_HD
-#endif
 
 #define BGV_UNROLL _Pragma("unroll")
 #define BGV_NO_UNROLL _Pragma("unroll 1")

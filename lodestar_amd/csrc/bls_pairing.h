@@ -224,7 +224,6 @@ BGV_MILLER_ATTR lzf12 lz_miller_add_step(const lzf12& f, lz_tpt& t, const lz_jq&
 // The per-set Miller loop of the blst batch equation (maybeBatch.ts:18-25 ->
 // verifyMultipleAggregateSignatures): e(r_i pk_i, H(m_i)); the signature side
 // e(-G1, sum r_i sig_i) is one team loop per device group (bls_team.h).
-#ifndef BGV_MILLER_EAGER
 // P and Q are read from memory: the Jacobian-Q constants of the 5 addition steps (16 Fp,
 // 224 VGPRs) are recomputed there from Q and P (~19 products per step) instead of staying
 // live across the 63 doubling steps, where the registers hold f, T and the step's
@@ -251,34 +250,6 @@ BGV_MILLER_LOOP_ATTR fp12_t miller_loop1m(const g1_jac* pm, const g2_jac* qm) {
   return fp12_conj(lz12_out(f));
 }
 BGV_HD fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) { return miller_loop1m(&p, &q); }
-#else
-BGV_MILLER_LOOP_ATTR fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) {
-  const miller_p P = miller_p_make(p);
-#ifndef BGV_MILLER_JQ_RECOMPUTE
-  const miller_jq c = miller_jq_make(q, P);
-#endif
-  g2_jac t = q;
-  fp2_t l0, l1, l3;
-  const uint64_t X = BGV_X_ABS;
-  miller_dbl(t, &l0, &l1, &l3, P);
-  fp12_t f = fp12_from_line(l0, l1, l3);
-  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
-    if ((X >> (i + 1)) & 1) {
-#ifdef BGV_MILLER_JQ_RECOMPUTE
-      // the Jacobian-Q constants for the 5 addition steps only: 112 fewer live VGPRs
-      // across the 63 doubling steps, 5 x 17 Fp products recomputed
-      const miller_jq c = miller_jq_make(q, P);
-#endif
-      miller_add_jq(t, &l0, &l1, &l3, c);
-      f = fp12_mul_line(f, l0, l1, l3);
-    }
-    f = fp12_sqr(f);
-    miller_dbl(t, &l0, &l1, &l3, P);
-    f = fp12_mul_line(f, l0, l1, l3);
-  }
-  return fp12_conj(f);
-}
-#endif
 
 // a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
 BGV_NOINLINE fp12_t cyclotomic_pow_x(const fp12_t& a) {
