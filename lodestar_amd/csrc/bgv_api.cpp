@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <unordered_map>
 #include <deque>
 #include <mutex>
 #include <shared_mutex>
@@ -172,6 +173,7 @@ struct Layout {
   std::vector<char> group_shared;        // group holds sets of more than one job
   std::vector<uint32_t> idx;             // concatenated pubkey indices
   std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
+  std::vector<uint32_t> uniq;            // first slot of each distinct signing root (hash_to_G2 once)
 };
 
 struct Builder {
@@ -179,6 +181,9 @@ struct Builder {
   bool open = false;  // a group is open for appending
   uint32_t open_group = 0;
   int open_job = -1;
+  // signing root -> its first slot, keyed by the root's first 8 bytes (a SHA-256 output); a
+  // key collision between different roots only costs one extra hash
+  std::unordered_map<uint64_t, uint32_t> first_root;
   explicit Builder(Layout& l) : L(l) {}
 
   void close_group() { open = false; }
@@ -198,6 +203,7 @@ struct Builder {
     bgv_dslot s;
     memset(&s, 0, sizeof(s));
     s.flags = BGV_SLOT_PAD;
+    s.hsrc = (uint32_t)L.slots.size();
     L.slots.push_back(s);
     L.slot_set.push_back(-1);
   }
@@ -228,6 +234,16 @@ struct Builder {
     }
     memcpy(s.msg, st.msg, 32);
     if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
+    const uint32_t self = (uint32_t)L.slots.size();
+    uint64_t key;
+    memcpy(&key, st.msg, 8);
+    const auto it = first_root.emplace(key, self).first;
+    if (it->second != self && memcmp(L.slots[it->second].msg, st.msg, 32) == 0) {
+      s.hsrc = it->second;  // same root as an earlier slot of this call
+    } else {
+      s.hsrc = self;
+      L.uniq.push_back(self);
+    }
     L.slots.push_back(s);
     L.slot_set.push_back((int32_t)set_index);
     g.n_slots++;
@@ -680,23 +696,24 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   double t_merge = 0, t_tok = 0, t_sets = 0, t_pass1 = 0, t_post = 0, t_retry = 0;
   // merge the calls' layouts
   uint32_t nslots = 0, ngroups = 0;
-  size_t nidx = 0, npkb = 0;
+  size_t nidx = 0, npkb = 0, nuniq = 0;
   for (Call* call : calls) {
     call->slot_base = nslots;
     nslots += (uint32_t)call->L.slots.size();
     ngroups += (uint32_t)call->L.groups.size();
     nidx += call->L.idx.size();
     npkb += call->L.pkb.size();
+    nuniq += call->L.uniq.size();
   }
   HIPCHK(hipSetDevice(d.id));
   int rc;
   if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
-      (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx, 1))) ||
+      (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx + nuniq, 1))) ||
       (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
     return rc;
   HIPCHK(x.h_slots.reserve(nslots));
   HIPCHK(x.h_groups.reserve(std::max<size_t>(ngroups, 1)));
-  HIPCHK(x.h_idx.reserve(nidx));
+  HIPCHK(x.h_idx.reserve(nidx + nuniq));  // pubkey indices, then the hashed slots (b.uniq)
   HIPCHK(x.h_pkb.reserve(npkb));
   HIPCHK(x.h_ss.reserve(nslots));
   HIPCHK(x.h_ps.reserve(nslots));
@@ -709,6 +726,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     for (Call* call : calls) {
       const uint32_t ib = (uint32_t)ni, pb = (uint32_t)(npb / 96), gb = (uint32_t)ng;
       for (bgv_dslot s : call->L.slots) {
+        s.hsrc += call->slot_base;
         if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
         if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
         if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
@@ -721,6 +739,9 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       if (!call->L.pkb.empty()) memcpy(x.h_pkb.p + npb, call->L.pkb.data(), call->L.pkb.size());
       npb += call->L.pkb.size();
     }
+    uint32_t* u = x.h_idx.p + nidx;
+    for (Call* call : calls)
+      for (uint32_t v : call->L.uniq) *u++ = v + call->slot_base;
   }
   std::vector<uint64_t> sc(nslots);
   fill_scalars(c, sc.data(), nslots);
@@ -735,10 +756,12 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   if (c->fault_inject) HIPCHK(hipErrorLaunchFailure);
   HIPCHK(hipMemcpyAsync(x.d_slots, slots, sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x.main));
   HIPCHK(hipMemcpyAsync(x.d_groups, groups, sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x.main));
-  if (nidx) HIPCHK(hipMemcpyAsync(x.d_idx, x.h_idx.p, 4 * nidx, hipMemcpyHostToDevice, x.main));
+  if (nidx + nuniq) HIPCHK(hipMemcpyAsync(x.d_idx, x.h_idx.p, 4 * (nidx + nuniq), hipMemcpyHostToDevice, x.main));
   if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, x.h_pkb.p, npkb, hipMemcpyHostToDevice, x.main));
   bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
   b.max_npk = max_npk;
+  b.uniq = x.d_idx + nidx;
+  b.nuniq = (uint32_t)nuniq;
   bgv_streams S{x.main, prof ? x.kev : nullptr};
   bgv_streams SC{x.close, prof ? x.kev : nullptr};
   int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;

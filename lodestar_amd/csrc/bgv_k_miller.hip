@@ -36,7 +36,7 @@ __global__ void BGV_KATTR k_miller(const bgv_dslot* __restrict__ slots, uint32_t
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < nslots) {
     fp12_t r = fp12_one();
-    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1m(rpk + s, h + s);
+    if (slot_live(slots[s], sig_status[s], pk_status[s])) r = miller_loop1m(rpk + s, h + slots[s].hsrc);
     f[s] = r;
   } else if (s - nslots < ngroups) {
     gpair[s - nslots] = group_pair(gsum + (s - nslots));
@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
   const fp_t* qsrc;
   if (set_pair) {
     live = slot_live(slots[uu], sig_status[uu], pk_status[uu]);
-    qsrc = reinterpret_cast<const fp_t*>(h + uu);
+    qsrc = reinterpret_cast<const fp_t*>(h + slots[uu].hsrc);  // H of the slot's signing root
   } else {
     qsrc = reinterpret_cast<const fp_t*>(gsum + (uu - nslots));
     live = !jac_is_inf(gsum[uu - nslots]);

@@ -369,13 +369,21 @@ __global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint3
                                       int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
                                       const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                       const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg,
+                                      const uint32_t* __restrict__ uniq, uint32_t nuniq) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  // hash first: the longest task starts earliest.  With uniq, lane u hashes the u-th distinct
+  // signing root (slot uniq[u]); lanes past nuniq -- whole waves of them -- exit at once.
+  if (blockIdx.y == 0) {
+    if (uniq) {
+      if (s < nuniq) task_hash(uniq[s], slots, h);
+    } else if (s < nslots) {
+      task_hash(s, slots, h);
+    }
+    return;
+  }
   if (s >= nslots) return;
-  // hash first: the longest task starts earliest
-  if (blockIdx.y == 0)
-    task_hash(s, slots, h);
-  else if (blockIdx.y == 1)
+  if (blockIdx.y == 1)
     task_sig(s, slots, rsig, sig_status);
   else
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
@@ -420,7 +428,7 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   } else {
     hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                       tree ? b.pk_agg : nullptr);
+                       tree ? b.pk_agg : nullptr, b.uniq, b.nuniq);
   }
   BGV_MARK(1);
   return hipGetLastError();

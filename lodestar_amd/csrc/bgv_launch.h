@@ -21,6 +21,10 @@ struct bgv_cache_entry;
 struct bgv_dev_batch {
   uint32_t nslots, ngroups;
   uint32_t max_npk;  // largest n_pk of any slot (k_pk_agg runs only when a set reaches BGV_PK_TREE_MIN)
+  // slots whose H(msg) the bulk k_prep computes (the first slot of each distinct signing root of
+  // a call); the other slots read H at their hsrc.  Null: every slot hashes its own message.
+  const uint32_t* uniq;
+  uint32_t nuniq;
   const bgv_dslot* slots;
   const bgv_dgroup* groups;
   const uint32_t* pk_idx;

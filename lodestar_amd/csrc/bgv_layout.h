@@ -24,7 +24,8 @@ struct bgv_dslot {
   uint32_t sig_len; // length of the signature bytes as received (96 is the only valid size)
   uint64_t scalar;  // nonzero 64-bit batch randomizer r
   uint32_t group;   // device group id
-  uint32_t pad_;
+  uint32_t hsrc;    // slot whose H(msg) this slot uses: the first slot of its call with the same
+                    // signing root (its own index for that first slot and for pads)
   uint8_t msg[32];  // signing root
   uint8_t sig[96];  // compressed G2 signature (untrusted wire bytes)
 };

@@ -78,10 +78,12 @@ def test_config2_aggregates(big):
     assert c.verify_jobs(jobs, native.MODE_WORKER) == [1, 1, 0, 1, 1, 1, 1, 1]
 
 
-def _gossip(c, sks, n, base, seed):
+def _gossip(c, sks, n, base, seed, committee=1):
+    """n one-set jobs, 1 % corrupted; `committee` consecutive sets share one signing root
+    (mainnet-shaped: one root per committee) -- 1 = distinct roots."""
     from lodestar_amd import native
     key_of = [(base + i * 7919) % len(sks) for i in range(n)]
-    msgs = [hashlib.sha256(b"lodestar-bench" + i.to_bytes(4, "little")).digest() for i in range(n)]
+    msgs = [hashlib.sha256(b"lodestar-bench" + (i // committee).to_bytes(4, "little")).digest() for i in range(n)]
     sigs = c.sign(b"".join(sk_bytes(sks[k]) for k in key_of), b"".join(msgs))
     sigs = [sigs[96 * i:96 * i + 96] for i in range(n)]
     expect = [1] * n
@@ -123,6 +125,24 @@ def _block_import_sets(c, sks, att_size=128):
     agg = [sum(sks[k] for k in g) % R for g in groups]
     sigs = c.sign(b"".join(sk_bytes(k) for k in agg), b"".join(msgs))
     return [native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=g) for i, g in enumerate(groups)], groups
+
+
+@pytest.mark.parametrize("n,committee", [(20000, 125), (20000, 1), (96, 16)])
+def test_mainnet_shaped_roots(big, n, committee):
+    """Sets sharing signing roots: the bulk k_prep hashes each distinct root of a call once
+    (bgv_dslot.hsrc / b.uniq) and every slot's Miller loop reads its root's H; the latency
+    path (96 sets) hashes every slot.  A corrupted message is a root of its own.  Verdicts by
+    construction, both modes."""
+    from lodestar_amd import native
+    c, sks = big
+    sets, expect = _gossip(c, sks, n, 777, 0x5EED + committee, committee)
+    assert c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER) == expect
+    if n <= 1024:
+        assert c.verify_jobs([([s], True) for s in sets], native.MODE_PER_JOB) == expect
+    # one non-batchable job of the first 128 sets: valid iff none of them is corrupted
+    head = sets[:128]
+    want = -1 if -1 in expect[:128] else (0 if 0 in expect[:128] else 1)
+    assert c.verify_jobs([(head, False)], native.MODE_WORKER) == [want]
 
 
 def test_config3_block_import_full_shape(big):
