@@ -177,11 +177,11 @@ BGV_HD lz<LA + lz_sub_t<LB, VB>::K.maxl, VA + lz_sub_t<LB, VB>::K.k> lz_sub(cons
   return r;
 }
 
-// k p - b
+// k p - b: at most k p (b = 0), so the value bound is k + 1
 template <uint64_t LB, uint64_t VB>
-BGV_HD lz<lz_sub_t<LB, VB>::K.maxl, lz_sub_t<LB, VB>::K.k> lz_neg(const lz<LB, VB>& b) {
+BGV_HD lz<lz_sub_t<LB, VB>::K.maxl, lz_sub_t<LB, VB>::K.k + 1> lz_neg(const lz<LB, VB>& b) {
   constexpr lzc::kp K = lzc::make_kp(LB, VB);
-  lz<K.maxl, K.k> r;
+  lz<K.maxl, K.k + 1> r;
   BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = K.v[i] - b.v[i];
   LZ_CHECK(r, "neg");
   return r;
