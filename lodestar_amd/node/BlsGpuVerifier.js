@@ -250,6 +250,19 @@ class BlsGpuVerifier {
 
   // ---- SURVEY 8(f) entry points (synchronous; low volume beside verifySignatureSets) ----
 
+  /** Light-client sync-aggregate check, isValidBlsAggregate (light-client/src/validation.ts:152-176):
+   * PublicKey.aggregate(publicKeys) (throws on an empty list), then
+   * Signature.fromBytes(signature, undefined, true).verify(aggPubkey, message) as one
+   * non-batchable aggregate set: an undecodable or non-G2 signature throws with its BLST code,
+   * an infinity aggregate verifies false. */
+  async isValidBlsAggregate(publicKeys, message, signature) {
+    if (publicKeys.length === 0) throw Error("EMPTY_AGGREGATE_ARRAY");
+    return this.verifySignatureSets(
+      [{type: SignatureSetType.aggregate, pubkeys: publicKeys, signingRoot: message, signature}],
+      {batchable: false}
+    );
+  }
+
   /** bls.Signature.aggregate(sigs.map((s) => Signature.fromBytes(s, undefined, true))).toBytes()
    * (chain/opPools/attestationPool.ts:184-187): throws Error(BLST code) like the dependency. */
   aggregateSignatures(sigs) {

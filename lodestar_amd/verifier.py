@@ -142,6 +142,19 @@ class BlsGpuVerifier:
             raise Exception("Empty results array")
         return all(r is True for r in results)
 
+    async def is_valid_bls_aggregate(self, public_keys: Sequence[PublicKey], message: bytes,
+                                     signature: bytes) -> bool:
+        """Light-client sync-aggregate check, isValidBlsAggregate (light-client/src/validation.ts:
+        152-176): PublicKey.aggregate(publicKeys), which throws on an empty list, then
+        Signature.fromBytes(signature, undefined, true).verify(aggPubkey, message).  One
+        non-batchable aggregate set on the device: an undecodable or non-G2 signature raises with
+        its BLST code, an infinity aggregate verifies false (core verify of a one-set job)."""
+        if len(public_keys) == 0:
+            raise native.BlsGpuError(native.BGV_E_EMPTY_AGGREGATE)
+        s = ISignatureSet(SignatureSetType.aggregate, signing_root=message, signature=signature,
+                          pubkeys=list(public_keys))
+        return await self.verify_signature_sets([s], VerifySignatureOpts(batchable=False))
+
     async def close(self):
         if self.buffered and self.buffered.get("timer"):
             self.buffered["timer"].cancel()

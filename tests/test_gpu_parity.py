@@ -238,3 +238,37 @@ def test_deposits_verify_golden(ctx):
     got = ctx.deposits_verify([bytes.fromhex(c["pk"]) for c in cases], [bytes.fromhex(c["msg"]) for c in cases],
                               [bytes.fromhex(c["sig"]) for c in cases])
     assert got == [c["expect"] for c in cases]
+
+
+def test_light_client_is_valid_bls_aggregate(ctx):
+    """light-client/src/validation.ts:152-176 isValidBlsAggregate on BlsGpuVerifier: a sync
+    aggregate over golden keys (96-B uncompressed pubkeys, as the light client holds PublicKey
+    objects) verifies; a wrong root is false; an empty key list and an undecodable signature raise
+    with the dependency's codes; the infinity aggregate (k and -k) verifies false."""
+    from lodestar_amd import native
+    from lodestar_amd.verifier import BlsGpuVerifier
+    from oracle import bls12381 as o  # checker only
+    keys = load("keys.json")
+    n = min(16, len(keys["sk"]))
+    sks = [int(k, 16) for k in keys["sk"][:n]]
+    pks = [bytes.fromhex(k) for k in keys["pk_uncompressed"][:n]]
+    root = hashlib.sha256(b"lc-sync-aggregate").digest()
+    agg_sk = sum(sks) % o.R
+    sig = ctx.sign(agg_sk.to_bytes(32, "big"), root)
+
+    async def run():
+        v = BlsGpuVerifier(ctx)
+        assert await v.is_valid_bls_aggregate(pks, root, sig) is True
+        assert await v.is_valid_bls_aggregate(pks, hashlib.sha256(b"other").digest(), sig) is False
+        assert await v.is_valid_bls_aggregate(pks[:-1], root, sig) is False
+        with pytest.raises(native.BlsGpuError) as e:
+            await v.is_valid_bls_aggregate([], root, sig)
+        assert e.value.code == native.BGV_E_EMPTY_AGGREGATE
+        with pytest.raises(native.BlsGpuError) as e:
+            await v.is_valid_bls_aggregate(pks, root, bytes([sig[0] & 0x7F]) + sig[1:])
+        assert e.value.code == native.BLST_BAD_ENCODING
+        neg = o.g1_serialize(o.sk_to_pk(o.R - sks[0]))
+        assert await v.is_valid_bls_aggregate([pks[0], neg], root, sig) is False
+        await v.close()
+
+    asyncio.run(run())
