@@ -71,6 +71,14 @@ static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 // k_prep_a / k_prep_b and the team Miller loop instead of one lane per set and task, which
 // wins while the chip would otherwise sit mostly idle (one lane per set runs ~13 ms in
 // k_miller however small the call).  BGV_LATENCY_MAX overrides (0 disables).
+// group closing on 12-lane teams (k_final12) instead of 16 (BGV_FINAL12=0: k_final)
+static inline bool bgv_final12() {
+  static const bool v = [] {
+    const char* e = getenv("BGV_FINAL12");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
 static inline uint32_t bgv_latency_max() {
   static const uint32_t v = [] {
     const char* e = getenv("BGV_LATENCY_MAX");

@@ -11,11 +11,14 @@
 static __constant__ fp2_t kTeamFrob1[6] = BGV_FROB1;
 static __constant__ fp_t kTeamFrob2[6] = BGV_FROB2;
 
-struct tm_dev_ops {
+// T = lanes per team: 16 (lanes 12..15 duplicate 8..11; the team Miller loop's rounds use
+// all 16) or 12 (k_final: five teams per wave)
+template <int T>
+struct tm_dev_ops_t {
   fp_t* A;  // this team's 12 + 12 LDS slots
   fp_t* B;
-  int c;   // lane within the team, 0..15
-  int cc;  // component computed by this lane (lanes 12..15 duplicate 8..11)
+  int c;   // lane within the team, 0..T-1
+  int cc;  // component computed by this lane
   __device__ fp_t mul(const fp_t& x, const fp_t& y) {
     if (c < BGV_TEAM_COMPS) {
       A[c] = x;
@@ -53,8 +56,9 @@ struct tm_dev_ops {
   __device__ bool is_fp6(const fp_t& x) {
     const bool bad = c < BGV_TEAM_COMPS && ((cc >> 1) & 1) && !fp_is_zero(x);
     const uint64_t m = __ballot(bad);
-    return ((m >> (threadIdx.x & ~(BGV_TEAM - 1))) & 0xffffu) == 0;
+    return ((m >> ((threadIdx.x / T) * T)) & ((1ull << T) - 1)) == 0;
   }
 };
+using tm_dev_ops = tm_dev_ops_t<BGV_TEAM>;
 
 
