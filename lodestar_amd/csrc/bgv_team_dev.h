@@ -1,6 +1,7 @@
 // Device side of a team (bls_team.h): the LDS exchange of the coefficient-parallel Fp12
 // operations, shared by the group closing (bgv_k_final.hip) and the team Miller loop
-// (bgv_k_miller.hip).  One team = 16 lanes of a 64-lane block; BGV_FINAL_TEAMS per block.
+// (bgv_k_miller.hip).  One team = 16 lanes of a 64-lane block, BGV_FINAL_TEAMS per block
+// (k_final12: 12 lanes, five teams per block).
 #pragma once
 #include "bgv_device.h"
 
