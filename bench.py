@@ -328,17 +328,19 @@ def super_batch_calls(steps, nsets, dispatchers=2, max_slots=163840):
     return best
 
 
-def stream_window(step, expect, warmup, steps, inflight):
+def stream_window(step, expect, warmup, steps, inflight, settle_s=0.0, boundary=1):
     """Calls stream continuously, `inflight` outstanding (the pool's concurrent jobs).  The
-    timed window runs from the warmup-th completion to the (warmup + steps)-th completion,
-    so exactly `steps` calls (steps x nsets sets) complete inside it, with the device busy
-    on both sides of it; feeding stops once the window is complete and the calls still in
-    flight drain untimed."""
+    timed window runs from the w-th completion to the (w + steps)-th completion, so exactly
+    `steps` calls (steps x nsets sets) complete inside it, with the device busy on both sides
+    of it; feeding stops once the window is complete and the calls still in flight drain
+    untimed.  w is the first multiple of `boundary` that is >= `warmup` and completes at
+    least `settle_s` seconds after the stream started (the clock settles at the device's
+    power limit within ~0.3 s of full load; profiles/r02s3/warm/)."""
     import threading
     lock = threading.Lock()
-    st = {"submitted": 0, "limit": None}
+    st = {"submitted": 0, "limit": None, "warm": 0 if warmup == 0 and settle_s <= 0 else None}
     done, errors = [], []
-    target = warmup + steps
+    t_begin = time.perf_counter()
 
     def worker():
         while True:
@@ -357,10 +359,13 @@ def stream_window(step, expect, warmup, steps, inflight):
             t = time.perf_counter()
             with lock:
                 done.append((t, t - ts, s, got == expect))
-                if len(done) >= target and st["limit"] is None:
+                n = len(done)
+                if (st["warm"] is None and n >= warmup and n % boundary == 0
+                        and t - t_begin >= settle_s):
+                    st["warm"] = n
+                if st["warm"] is not None and n >= st["warm"] + steps and st["limit"] is None:
                     st["limit"] = st["submitted"]
 
-    t_begin = time.perf_counter()
     threads = [threading.Thread(target=worker, daemon=True) for _ in range(inflight)]
     for t in threads:
         t.start()
@@ -369,12 +374,14 @@ def stream_window(step, expect, warmup, steps, inflight):
     if errors:
         raise errors[0]
     done.sort(key=lambda d: d[0])
-    if len(done) < target or not all(d[3] for d in done):
+    warmup = st["warm"]
+    target = (warmup or 0) + steps
+    if warmup is None or len(done) < target or not all(d[3] for d in done):
         raise SystemExit("verdict mismatch")
     t0 = done[warmup - 1][0] if warmup else t_begin
     window = done[warmup:target]
     return {"elapsed": window[-1][0] - t0, "latencies": [d[1] for d in window], "stats": [d[2] for d in window],
-            "calls_total": len(done)}
+            "calls_total": len(done), "warm_calls": warmup}
 
 
 # PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
@@ -421,6 +428,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum host-CPU time of the cpu_baseline sample")
     ap.add_argument("--no-block-import", action="store_true", help="skip the config-3 latency measurement")
     ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of corrupted sets (config 4: 1%%)")
+    ap.add_argument("--settle-s", type=float, default=0.6,
+                    help="untimed full-load seconds before the window (on top of --warmup calls) so the window runs "
+                         "at the power-settled clock; 0 disables")
     ap.add_argument("--calls-per-batch", type=int, default=0,
                     help="calls merged per device super-batch (default: the largest divisor of --steps "
                          "with <= 163840 sets)")
@@ -458,13 +468,18 @@ def main():
     # so every super-batch fills to B calls (restored after the timed region)
     ndisp = int(os.environ.get("BGV_DISPATCHERS", "2"))
     bcalls = args.calls_per_batch or super_batch_calls(args.steps, args.nsets, ndisp)
-    # the window opens on a super-batch boundary: at least `warmup` calls complete before it
+    # the window opens on a super-batch boundary: at least `warmup` calls complete before it,
+    # and at least --settle-s seconds of full load (the device's clock settles at its power
+    # limit within ~0.3 s; a window inside that boost phase reads up to ~20 % high,
+    # profiles/r02s3/warm/)
     warm_calls = -(-args.warmup // bcalls) * bcalls
     ctx.set_batching(bcalls * args.nsets, 200000, 200000)
     ctx.profile(1)
     barrier()
     cuda_sync()
-    win = stream_window(step, expect, warm_calls, args.steps, max(args.inflight, 3 * bcalls))
+    win = stream_window(step, expect, warm_calls, args.steps, max(args.inflight, 3 * bcalls),
+                        settle_s=args.settle_s, boundary=bcalls)
+    warm_calls = win["warm_calls"]
     cuda_sync()
     barrier()
     ctx.set_batching(131072, 2000, 200)
@@ -539,10 +554,11 @@ def main():
                        "parallelism": "dp%d (independent batches per GPU)" % world},
             "timing": "steady state: calls stream with the given number in flight; the window runs from the "
                       "%d-th to the %d-th completed call (exactly %d calls inside; the %d warmup steps are the "
-                      "first %d completions, rounded up to whole super-batches), super-batches of %d calls so both "
+                      "first %d completions, rounded up to whole super-batches and extended to >= %.1f s of "
+                      "full load so the window runs at the power-settled clock), super-batches of %d calls so both "
                       "edges fall on batch boundaries; %d calls completed in all"
-                      % (warm_calls, warm_calls + args.steps, args.steps, args.warmup, warm_calls, bcalls,
-                         win["calls_total"]),
+                      % (warm_calls, warm_calls + args.steps, args.steps, args.warmup, warm_calls, args.settle_s,
+                         bcalls, win["calls_total"]),
             "kernel_ms_per_launch": avg,
             "retries_per_step": statistics.mean(s.batch_retries for s in stats),
             "call_device_ms": statistics.mean(s.device_ms for s in stats),
