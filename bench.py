@@ -6,22 +6,34 @@ A step = one pass of the hot path over one synthetic batch: bgv_verify of 8192
 signature sets (config 4: gossip shape, 8192 batchable one-set jobs, 1 %
 corrupted so the batch-fail -> per-job retry path runs), inputs already resident
 (pubkey cache on the device, set records in host memory as the C-ABI takes them).
-For N > 1 (torchrun) every rank verifies its own 8192-set batches on its own GPU
-(sets shard with no data-path exchange: scaling "weak"); the slowest rank's time
-is the job time.  Verdicts of every step are checked against the expected codes
-(known by construction, the corruption classes pinned by tests/test_gpu_parity.py).
+
+N GPUs: one process per GPU.  Under torchrun the ranks come from the environment; a plain
+`python bench.py --gpus N` starts the N rank processes itself (from this parent, which never
+touches the GPU) and fails loudly if the ranks that ran differ from --gpus.  Every rank
+verifies its own 8192-set batches on its own GPU (jobs shard with no data-path exchange:
+scaling "weak"); the slowest rank's time is the job time.  Verdicts of every step are checked
+against the expected codes (known by construction, the corruption classes pinned by
+tests/test_gpu_parity.py).  The process group is RCCL ("nccl") when the ranks drive distinct
+GPUs, gloo for the one-GPU rehearsal (BGV_BENCH_DEVICE) and on CPU.
 
 The JSON line carries:
   roofline     integer-VALU roofline of the dominant kernel: algorithmic u32 MACs
                (Fp-mul-eq counted in profiles/opcounts.json x 288) / its HIP-event time,
                against the gfx950 peak v_mad_u64_u32 rate (16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz)
-  cpu_baseline the C++ CPU restatement (oracle/cpu, worker-pool policy, up to 16 threads) on a
-               bounded sample of the same batch
+  epoch_sweep  config 5 at N GPUs: 2^20 single sets over a replicated 2^20-key device cache
+               (2048 committee roots), one job split over the ranks; each rank reduces its shard
+               to one Fp12 Miller-loop product (bgv_verify_partial), the partials are
+               all-gathered (RCCL over xGMI at N > 1) and one final exponentiation decides
+  cpu_baseline the C++ CPU restatement (oracle/cpu, BlsMultiThreadWorkerPool policy) on a
+               bounded sample of the same batch: 16 threads on 16 distinct cores, 16 threads on
+               8 SMT core pairs, all affinity threads (os.cpus().length, poolSize.ts:7), and the
+               whole-host pool derived from them (the box's cgroup quota caps what one run can
+               use); config 1 on one core
   block_import config 3 of BASELINE.json, measured after the timed region: p50 latency of one
                non-batchable 131-set call (randao + 128 attestations x 128 keys + 512-key sync
                aggregate + proposer), one call at a time
   aggregates_1024x128  config 2, also after the timed region: sets/s of 1024-set calls of
-               128-key aggregates (8 batchable jobs each), 32 calls in flight
+               128-key aggregates (8 batchable jobs each), 126 calls in flight
 """
 import argparse
 import hashlib
@@ -60,24 +72,63 @@ def dist_env():
     return rank, world, local
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without torchrun: N rank processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*
+    as torchrun sets them), started from this parent before anything touches the GPU.
+    Returns the first nonzero exit status (0 when every rank succeeded)."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
 class Barrier:
-    def __init__(self, world):
+    """Process group of the ranks: barrier, max over ranks, the collective of the epoch
+    sweep.  RCCL ("nccl") when the ranks drive distinct GPUs; gloo for the one-GPU
+    rehearsal (BGV_BENCH_DEVICE: RCCL refuses two ranks on one device) and on CPU."""
+
+    def __init__(self, world, local=0):
         self.world = world
         self.dist = None
+        self.dev = None
+        self.backend = None
         if world > 1:
+            import torch
             import torch.distributed as dist
-            dist.init_process_group("gloo", init_method="env://")
+            backend = os.environ.get("BGV_BENCH_BACKEND")
+            if backend is None:
+                backend = "nccl" if ("BGV_BENCH_DEVICE" not in os.environ and torch.cuda.is_available()) else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                self.dev = torch.device("cuda", local)
+            dist.init_process_group(backend, init_method="env://")
             self.dist = dist
+            self.backend = backend
 
     def __call__(self):
         if self.dist:
-            self.dist.barrier()
+            if getattr(self, "dev", None) is not None:
+                self.dist.barrier(device_ids=[self.dev.index])
+            else:
+                self.dist.barrier()
 
     def max(self, v: float) -> float:
         if not self.dist:
             return v
         import torch
-        t = torch.tensor([v], dtype=torch.float64)
+        t = torch.tensor([v], dtype=torch.float64, device=getattr(self, "dev", None) or "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -244,7 +295,8 @@ def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
 
 
 def host_cpu():
-    """nproc, model name and clock of the host the CPU leg runs on (/proc/cpuinfo)."""
+    """nproc, model name, clock, affinity and the cgroup CPU quota of the host the CPU leg
+    runs on (/proc/cpuinfo, /sys/fs/cgroup/cpu.max)."""
     model, mhz = "unknown", None
     try:
         with open("/proc/cpuinfo") as f:
@@ -261,37 +313,109 @@ def host_cpu():
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = os.cpu_count()
-    return {"nproc": os.cpu_count(), "affinity": affinity, "model": model, "mhz": mhz}
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": affinity, "model": model, "mhz": mhz, "cgroup_cpus": quota,
+            "physical_cores": len(core_groups())}
+
+
+def core_groups():
+    """Logical CPUs of this process's affinity grouped by physical core (SMT siblings,
+    /sys/devices/system/cpu/cpu*/topology/thread_siblings_list), in CPU order."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return [[c] for c in range(os.cpu_count() or 1)]
+    groups, seen = [], set()
+    for c in cpus:
+        if c in seen:
+            continue
+        sib = [c]
+        try:
+            txt = open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c).read().strip()
+            sib = []
+            for part in txt.split(","):
+                a, _, b = part.partition("-")
+                sib += list(range(int(a), int(b or a) + 1))
+            sib = [x for x in sib if x in cpus] or [c]
+        except OSError:
+            pass
+        seen.update(sib)
+        groups.append(sib)
+    return groups
+
+
+def timed_pool(blscpu, cj, expect, threads, min_seconds, cpus=None):
+    """blscpu.verify_jobs over cj with `threads` workers, repeated for >= min_seconds; the
+    workers inherit this thread's CPU affinity (set to `cpus` for the run).  Returns sets/s."""
+    old = None
+    if cpus is not None and hasattr(os, "sched_setaffinity"):
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, cpus)
+    try:
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            got = blscpu.verify_jobs(cj, 0, threads)
+            passes += 1
+            assert got == expect, "CPU restatement disagrees with the expected verdicts"
+            dt = time.perf_counter() - t0
+            if dt >= min_seconds:
+                return len(cj) * passes / dt, passes, dt
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
 
 
 def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
     """The C++ CPU restatement (oracle/cpu: blst's batch equation with 64-bit randomizers
     in width-5 wNAF, 8-pair Miller loops with shared squarings, mulx/adx Montgomery
-    products; BlsMultiThreadWorkerPool policy: packages of >= 128 sets over `threads`
-    workers, >= 16-job batch chunks, per-job retry) timed on this host on the first
-    `nsample` jobs of the same gossip batch, repeated until at least `min_seconds` of wall
-    time (a bounded sample: the default bench stays within minutes).  Workers = the host
-    threads this process may use, capped by BENCH_CPU_THREADS (16 = the GPU box's CPU share
-    per GPU; os.cpu_count() there reports the whole machine).  Also the config-1 row:
-    one 128-set job on ONE core (BlsSingleThreadVerifier, chain/bls/singleThread.ts:7-40,
-    maybeBatch.ts:16-39)."""
+    products; BlsMultiThreadWorkerPool policy: packages of >= 128 sets over the workers,
+    >= 16-job batch chunks, per-job retry) timed on this host on the first `nsample` jobs of
+    the same gossip batch, each row repeated for at least `min_seconds` (a bounded sample).
+
+    The reference sizes its pool at os.cpus().length (poolSize.ts:7).  The GPU box grants a
+    bench process a cgroup quota of 16 CPUs out of nproc = 256, so the whole-host pool cannot
+    run inside one measurement; it is derived from measured rows instead:
+      distinct16  16 workers pinned to 16 distinct physical cores (the primary row: `value`)
+      smt8x2      16 workers on 8 physical cores x 2 SMT siblings (per-core rate with SMT)
+      all         os.cpus().length workers on the whole affinity set (what poolSize.ts does;
+                  throttled to the quota here), on 4 copies of the sample so every worker
+                  has a 128-set package
+      host_pool   smt8x2 per-core rate x the host's physical cores: every core with both SMT
+                  threads at the clock 8 busy cores sustain (an all-core load clocks lower,
+                  so this favours the CPU)
+    Also the config-1 row: one 128-set job on ONE core (BlsSingleThreadVerifier,
+    chain/bls/singleThread.ts:7-40, maybeBatch.ts:16-39)."""
     from oracle.cpu import blscpu
     host = host_cpu()
-    threads = min(host["affinity"] or 1, int(os.environ.get("BENCH_CPU_THREADS", "16")))
     keys = sorted(set(key_of[:nsample]))
     pk = blscpu.sk_to_pk96(b"".join(interop_sk(k) for k in keys))
     pk_of = {k: pk[96 * i:96 * i + 96] for i, k in enumerate(keys)}
     cj = [([(pk_of[key_of[i]], s.msg, s.sig) for s in sets], b) for i, (sets, b) in enumerate(jobs[:nsample])]
-    passes = 0
-    t0 = time.perf_counter()
-    while True:
-        got = blscpu.verify_jobs(cj, 0, threads)
-        passes += 1
-        assert got == expect[:nsample], "CPU restatement disagrees with the expected verdicts"
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds:
-            break
-    nverified = nsample * passes
+    exp = expect[:nsample]
+    groups = core_groups()
+    rows = {}
+    distinct = [g[0] for g in groups[:16]]
+    r, passes, dt = timed_pool(blscpu, cj, exp, len(distinct), min_seconds, set(distinct))
+    rows["distinct16"] = {"value": r, "threads": len(distinct), "cpus": len(distinct), "physical_cores": len(distinct),
+                          "passes": passes, "seconds": dt}
+    pairs = [g[:2] for g in groups if len(g) >= 2][:8]
+    if len(pairs) == 8:
+        cpus = {c for g in pairs for c in g}
+        r2, passes2, dt2 = timed_pool(blscpu, cj, exp, 16, min_seconds, cpus)
+        rows["smt8x2"] = {"value": r2, "threads": 16, "cpus": 16, "physical_cores": 8, "passes": passes2,
+                          "seconds": dt2, "smt_gain_per_core": 2 * r2 / r}
+    nall = host["affinity"] or 1
+    r3, passes3, dt3 = timed_pool(blscpu, cj * 4, exp * 4, nall, min_seconds / 2)
+    rows["all"] = {"value": r3, "threads": nall, "passes": passes3, "seconds": dt3,
+                   "note": "os.cpus().length workers; the cgroup quota (%s CPUs) caps what they get" %
+                           host["cgroup_cpus"]}
+    per_core = rows["smt8x2"]["value"] / 8 if "smt8x2" in rows else r / 16
+    host_pool = per_core * len(groups)
     # config 1: 128 valid single sets as one non-batchable job, one thread
     valid = [i for i in range(nsample) if expect[i] == 1][:128]
     c1 = [([cj[i][0][0] for i in valid], False)]
@@ -303,17 +427,20 @@ def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
         d1 = time.perf_counter() - t1
         if d1 >= min(3.0, min_seconds):
             break
-    return {"value": nverified / dt, "unit": "sets/s", "cores": threads, "kind": "port",
-            "host": host,
+    return {"value": r, "unit": "sets/s", "cores": len(distinct), "kind": "port",
+            "host": host, "rows": rows,
+            "host_pool": {"value": host_pool, "unit": "sets/s", "cores": len(groups), "threads": host["affinity"],
+                          "derived": "smt8x2 per-core rate (%.0f sets/s) x %d physical cores" % (per_core, len(groups))},
             "config1_single_core": {"value": 128 * reps / d1, "unit": "sets/s", "cores": 1,
                                     "ms_per_job": 1e3 * d1 / reps,
                                     "sample": "%d x one 128-set job (batch equation), 1 thread" % reps},
-            "sample": "oracle/cpu/blscpu.cpp (C++ restatement with blst's algorithms, not blst itself): %d passes "
-                      "over the first %d jobs of the same 8192-set gossip batch (1%% corrupt, per-job retry), %d "
-                      "worker threads on %s (%s MHz, nproc %s), %.1f s; per-core %.0f sets/s (reference anchor: "
-                      "~0.9 ms per single verify with blst-native, metrics/lodestar.ts:477)"
-                      % (passes, nsample, threads, host["model"], host["mhz"], host["nproc"], dt,
-                         nverified / dt / threads)}
+            "sample": "oracle/cpu/blscpu.cpp (C++ restatement with blst's algorithms, not blst itself): the first %d "
+                      "jobs of the same 8192-set gossip batch (1%% corrupt, per-job retry), %d worker threads pinned "
+                      "to %d distinct physical cores of %s (%s MHz, nproc %s, cgroup quota %s CPUs), %.1f s; per-core "
+                      "%.0f sets/s (reference anchor: ~0.9 ms per single verify with blst-native, "
+                      "metrics/lodestar.ts:477)"
+                      % (nsample, len(distinct), len(distinct), host["model"], host["mhz"], host["nproc"],
+                         host["cgroup_cpus"], dt, r / len(distinct))}
 
 
 def super_batch_calls(steps, nsets, dispatchers=2, max_slots=163840):
@@ -384,6 +511,67 @@ def stream_window(step, expect, warmup, steps, inflight, settle_s=0.0, boundary=
             "calls_total": len(done), "warm_calls": warmup}
 
 
+EPOCH_SETS = 1 << 20
+EPOCH_COMMITTEE = 512  # 2048 committee roots over 2^20 sets
+
+
+def epoch_sweep(ctx, native, barrier, rank, world, nsets=EPOCH_SETS, committee=EPOCH_COMMITTEE):
+    """config 5: 2^20 single sets, set i signed by validator i over its
+    committee's root (2048 roots), pubkeys from the replicated 2^20-key device cache.  The
+    sweep is ONE job split over the ranks (ShardedVerify.one_job_from_shard): each rank's
+    contiguous shard becomes one bgv_verify_partial call (its Fp12 Miller-loop product, 576 B),
+    the partials are all-gathered over the process group (RCCL over xGMI at N > 1) and every
+    rank runs the single final exponentiation.  Timed: barrier + device sync on both sides,
+    max over ranks.  Then, untimed, two signatures of the last shard are swapped (both sets
+    invalid) and the same protocol must return false on every rank."""
+    from lodestar_amd.shard import ShardedVerify, shard_bounds
+    lo, hi = shard_bounds([1] * nsets, world)[rank]
+    t0 = time.perf_counter()
+    sks = [interop_sk(i) for i in range(nsets)]
+    if ctx.pubkeys_count() < nsets:
+        first = ctx.pubkeys_count()
+        ctx.keygen(b"".join(sks[first:]), cache_first=first, want_pubkeys=False)
+    roots = [hashlib.sha256(b"lodestar-epoch" + c.to_bytes(4, "little")).digest() for c in range(nsets // committee)]
+    msgs = b"".join(roots[i // committee] for i in range(lo, hi))
+    sigs = ctx.sign(b"".join(sks[lo:hi]), msgs)
+    del sks
+    packed = native.PackedSingleSets(msgs, sigs, range(lo, hi))
+    setup_s = time.perf_counter() - t0
+    sv = ShardedVerify(None, barrier.dist, final_fn=ctx.final_verify) if barrier.dist else None
+
+    def one_pass():
+        def shard():
+            return ctx.verify_partial_packed(packed, 0, hi - lo)
+        if sv is None:
+            p, sc, pc = shard()
+            if sc or pc:
+                return sc or (-6 if pc == 1 else pc)
+            return 1 if ctx.final_verify([p]) else 0
+        return sv.one_job_from_shard(shard, nsets)
+
+    assert one_pass() == 1, "epoch sweep: valid sweep rejected"  # warm (buffers sized)
+    barrier()
+    cuda_sync()
+    t1 = time.perf_counter()
+    code = one_pass()
+    cuda_sync()
+    barrier()
+    elapsed = barrier.max(time.perf_counter() - t1)
+    assert code == 1, "epoch sweep: verdict %r" % code
+    # corrupted: swap two signatures of the last rank's shard -> false on every rank
+    if rank == world - 1 and hi - lo >= 2:
+        a, b = packed._sig[0:96].copy(), packed._sig[96:192].copy()
+        packed._sig[0:96], packed._sig[96:192] = b, a
+    bad = one_pass()
+    assert bad == 0, "epoch sweep: corrupted sweep verdict %r" % bad
+    return {"config": "config5: 2^20 single sets over a replicated 2^20-key device cache, %d committee roots, one "
+                      "job split over %d rank(s): per-rank bgv_verify_partial (Fp12 Miller-loop product), all-gather "
+                      "of the 576-B partials (%s), one final exponentiation" %
+                      (nsets // committee, world, barrier.backend or "single rank: no collective"),
+            "sets": nsets, "sets_per_rank": hi - lo, "value": nsets / elapsed, "unit": "sets/s",
+            "ms": 1e3 * elapsed, "setup_s": setup_s, "verdicts": {"valid": code, "two_swapped_signatures": bad}}
+
+
 # PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
 TRAFFIC_FILE = os.path.join("profiles", "r02s3", "traffic.json")
 ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
@@ -434,9 +622,27 @@ def main():
     ap.add_argument("--calls-per-batch", type=int, default=0,
                     help="calls merged per device super-batch (default: the largest divisor of --steps "
                          "with <= 163840 sets)")
+    ap.add_argument("--no-epoch-sweep", action="store_true", help="skip the config-5 sweep leg")
+    ap.add_argument("--check-ranks", action="store_true",
+                    help="preflight: start the ranks, join the process group, print one line naming the ranks "
+                         "and the backend, exit (no GPU work)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     rank, world, local = dist_env()
-    barrier = Barrier(world)
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but %d rank(s) are running" % (args.gpus, world))
+    if args.check_ranks:
+        os.environ.setdefault("BGV_BENCH_BACKEND", "gloo")
+    barrier = Barrier(world, local)
+    if args.check_ranks:
+        barrier()
+        ranks = barrier.max(float(rank + 1))
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "ranks_joined": int(ranks), "backend": barrier.backend,
+                              "local_rank_of_rank0": local}), flush=True)
+        barrier.close()
+        return
 
     from lodestar_amd import native
     ctx = native.Context([local])
@@ -497,6 +703,7 @@ def main():
     if extras and args.nkeys >= 131072:
         agg = aggregate_throughput(ctx, native, args.nkeys)
         mainnet = mainnet_shaped_throughput(ctx, native, args.nkeys)
+    sweep = None if args.no_epoch_sweep else epoch_sweep(ctx, native, barrier, rank, world)
 
     if rank == 0:
         total_sets = args.nsets * args.steps * world
@@ -584,9 +791,17 @@ def main():
             line["aggregates_1024x128"] = agg
         if mainnet is not None:
             line["mainnet_shaped_roots"] = mainnet
+        if sweep is not None:
+            line["epoch_sweep"] = sweep
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            line["cpu_baseline"] = cpu_baseline(jobs, key_of, expect, min(args.nsets, args.cpu_sample),
-                                                args.cpu_seconds)
+            cb = cpu_baseline(jobs, key_of, expect, min(args.nsets, args.cpu_sample), args.cpu_seconds)
+            line["cpu_baseline"] = cb
+            # BASELINE.md publishes no number for this metric; the ratio the north star names
+            # (GPU sets/s over the host's whole blst-style worker pool) stands in
+            line["vs_baseline"] = line["value"] / cb["host_pool"]["value"]
+            line["vs_baseline_basis"] = ("value / cpu_baseline.host_pool (the C++ restatement's pool over all %d "
+                                         "physical cores of this host, derived from pinned rows)" %
+                                         cb["host_pool"]["cores"])
         print(json.dumps(line), flush=True)
     ctx.close()
     barrier.close()

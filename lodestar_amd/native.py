@@ -266,6 +266,15 @@ class Context:
         _check(self.lib.bgv_verify_partial(self._h, packed.sets, packed.nsets, out, codes))
         return out.raw, codes[0], codes[1]
 
+    def verify_partial_packed(self, packed: "PackedSingleSets", lo: int, hi: int) -> tuple:
+        """verify_partial over sets [lo, hi) of a PackedSingleSets (no per-set objects)."""
+        if not 0 <= lo <= hi <= packed.nsets:
+            raise ValueError("shard bounds out of range")
+        out = ctypes.create_string_buffer(576)
+        codes = (ctypes.c_int32 * 2)()
+        _check(self.lib.bgv_verify_partial(self._h, packed.ptr(lo), hi - lo, out, codes))
+        return out.raw, codes[0], codes[1]
+
     def final_verify(self, partials: Sequence[bytes]) -> bool:
         """Product of serialized partials and one final exponentiation == 1 (bgv_final_verify)."""
         v = ctypes.c_int32()
@@ -300,6 +309,37 @@ class SetSpec:
     @property
     def n_pk(self):
         return len(self.pk_indices) if self.pk_indices is not None else len(self.pk_bytes)
+
+
+class PackedSingleSets:
+    """n single-pubkey sets over contiguous buffers (no per-set Python objects): set i has
+    signing root msgs[32 i:32 i + 32], signature sigs[96 i:96 i + 96] and cached pubkey index
+    idx[i].  For bulk shards (the config-5 epoch sweep: 2^20 sets) where SetSpec lists would
+    cost seconds of host time.  `sets` / `nsets` / `slice(lo, hi)` feed bgv_verify_partial."""
+
+    def __init__(self, msgs: bytes, sigs: bytes, idx: Sequence[int]):
+        import numpy as np
+        n = len(idx)
+        if len(msgs) != 32 * n or len(sigs) != 96 * n:
+            raise ValueError("msgs / sigs sizes do not match the index count")
+        self._msg = np.frombuffer(bytes(msgs), dtype=np.uint8).copy()
+        self._sig = np.frombuffer(bytes(sigs), dtype=np.uint8).copy()
+        self._idx = np.asarray(idx, dtype=np.uint32).copy()
+        rec = np.dtype([("n_pk", "<u4"), ("sig_len", "<u4"), ("pk_indices", "<u8"), ("pk_bytes", "<u8"),
+                        ("msg", "<u8"), ("sig", "<u8")])
+        assert rec.itemsize == ctypes.sizeof(BgvSet)
+        arr = np.zeros(max(1, n), dtype=rec)
+        k = np.arange(n, dtype=np.uint64)
+        arr["n_pk"][:n] = 1
+        arr["sig_len"][:n] = 96
+        arr["pk_indices"][:n] = self._idx.ctypes.data + 4 * k
+        arr["msg"][:n] = self._msg.ctypes.data + 32 * k
+        arr["sig"][:n] = self._sig.ctypes.data + 96 * k
+        self._arr = arr
+        self.nsets = n
+
+    def ptr(self, lo: int = 0):
+        return ctypes.c_void_p(self._arr.ctypes.data + lo * ctypes.sizeof(BgvSet))
 
 
 class PackedCall:

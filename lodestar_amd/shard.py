@@ -29,6 +29,7 @@ an error marker and then raises.
 from typing import Callable, List, Optional, Sequence, Tuple
 
 BGV_E_DEVICE = 30
+BGV_E_EMPTY_SET = 21
 BLST_PK_IS_INFINITY = 6
 ONE_FP12 = bytes(47) + b"\x01" + bytes(528)  # canonical bytes of 1 in GT's Fp12
 
@@ -133,7 +134,9 @@ class ShardedVerify:
         return out
 
     def _fast(self, mine):
-        """Whole-call partial products: (codes or None, error).  None codes = verify per job."""
+        """Whole-call partial products: (codes or None, error).  None codes = verify per job.
+        A job with no sets rejects with BGV_E_EMPTY_SET ("Empty signature set",
+        maybeBatch.ts:29-31) as on the per-job path; it adds nothing to the partial."""
         sets = [s for ss, _ in mine for s in ss]
         try:
             partial, sc, pc = self.partial_fn(sets) if sets else (ONE_FP12, 0, 0)
@@ -151,25 +154,34 @@ class ShardedVerify:
             from .native import DeviceError
             return None, DeviceError("BGV_E_DEVICE on another rank")
         clean = all(struct.unpack("<iii", p[576:])[:2] == (0, 0) for p in parts)
+        ok_codes = [1 if ss else -BGV_E_EMPTY_SET for ss, _ in mine]
         if clean and self.final_fn([p[:576] for p in parts]):
-            return [1] * len(mine), None  # one final exponentiation for the whole call
+            return ok_codes, None  # one final exponentiation for the whole call
         if sc == 0 and pc == 0 and self.final_fn([partial]):
-            return [1] * len(mine), None  # this shard is clean: only failing shards retry
+            return ok_codes, None  # this shard is clean: only failing shards retry
         return None, None
 
     # --- one job --------------------------------------------------------------------
     def verify_one_job(self, sets: list) -> int:
         """One job's sets split over the ranks; Fp12 partials gathered, one final
         exponentiation.  Returns the job's code (1, 0 or -BLST error) on every rank."""
-        import struct
         world = self.dist.get_world_size(self.group)
         rank = self.dist.get_rank(self.group)
         if not sets:
-            return -21  # BGV_E_EMPTY_SET: "Empty signature set" (maybeBatch.ts:29-31)
+            return -BGV_E_EMPTY_SET  # "Empty signature set" (maybeBatch.ts:29-31)
         lo, hi = shard_bounds([1] * len(sets), world)[rank]
+        return self.one_job_from_shard(lambda: self.partial_fn(sets[lo:hi]) if hi > lo else (ONE_FP12, 0, 0),
+                                       len(sets))
+
+    def one_job_from_shard(self, shard_partial: Callable[[], tuple], nsets: int) -> int:
+        """The collective half of verify_one_job: this rank's shard_partial() ->
+        (576-B partial, sig_code, pk_code) is all-gathered (RCCL with the nccl backend) and
+        every rank runs the one final exponentiation.  Callers that hold their shard in
+        another form (native.PackedSingleSets: the config-5 sweep) use this directly."""
+        import struct
         err = None
         try:
-            partial, sc, pc = self.partial_fn(sets[lo:hi]) if hi > lo else (ONE_FP12, 0, 0)
+            partial, sc, pc = shard_partial()
             ok = 1
         except Exception as e:  # noqa: BLE001 -- joined the collective below, then re-raised
             partial, sc, pc, ok, err = ONE_FP12, 0, 0, 0, e
@@ -185,7 +197,7 @@ class ShardedVerify:
                 return s
         for _, p, _ in codes:  # then the first pubkey condition
             if p == 1:
-                return -BLST_PK_IS_INFINITY if len(sets) >= 2 else 0
+                return -BLST_PK_IS_INFINITY if nsets >= 2 else 0
             if p:
                 return p
         return 1 if self.final_fn([p[:576] for p in parts]) else 0

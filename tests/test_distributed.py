@@ -141,6 +141,39 @@ def _one_job_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _fast_path_worker(rank, world, port, q):
+    """fast_path=True with stand-in partials (as _one_job_worker): an empty job rejects with
+    BGV_E_EMPTY_SET (-21) as on the per-job path, whether the combined check passes or a
+    shard falls back to verify_fn."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def partial_fn(sets):
+            return (ONE if all(v for v, _, _ in sets) else BAD), 0, 0
+
+        def verify_fn(js):
+            return [(-21 if not ss else (1 if all(v for v, _, _ in ss) else 0)) for ss, _ in js]
+
+        sv = ShardedVerify(verify_fn, dist, partial_fn=partial_fn,
+                           final_fn=lambda ps: all(p == ONE for p in ps), fast_path=True)
+        good = ([(1, 0, 0)], True)
+        bad = ([(0, 0, 0)], True)
+        empty = ([], True)
+        out = {
+            "clean_with_empty": sv([good, empty, good, good, empty, good]) == [1, -21, 1, 1, -21, 1],
+            "failing_with_empty": sv([good, empty, good, bad, empty, good]) == [1, -21, 1, 0, -21, 1],
+            "only_empty": sv([empty, empty]) == [-21, -21],
+        }
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fast_path_empty_job():
+    for rank, ok in _spawn(_fast_path_worker):
+        assert all(ok.values()), (rank, ok)
+
+
 def _spawn(target, world=2):
     port = _free_port()
     ctx = mp.get_context("spawn")

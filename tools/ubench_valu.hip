@@ -92,6 +92,51 @@ __global__ void k_fma_f64(uint64_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = __double_as_longlong(s);
 }
 
+
+// simple 32-bit / 64-bit ops: is their issue cost 2 cycles (SIMD-32) with several waves per
+// SIMD, and 4 with one wave alone?  (v_add_f32 is the guide's 2-cycle reference)
+#define SIMPLE_KERNEL(NAME, ASM, T, INIT)                                                         \
+  __global__ void NAME(uint64_t* out, uint32_t seed) {                                          \
+    T a = (T)(seed + threadIdx.x);                                                              \
+    T c0 = INIT(0), c1 = INIT(1), c2 = INIT(2), c3 = INIT(3), c4 = INIT(4), c5 = INIT(5), c6 = INIT(6), \
+      c7 = INIT(7);                                                                             \
+    for (int i = 0; i < ITERS; ++i) {                                                           \
+      asm volatile(ASM : "+v"(c0) : "v"(a)); asm volatile(ASM : "+v"(c1) : "v"(a));             \
+      asm volatile(ASM : "+v"(c2) : "v"(a)); asm volatile(ASM : "+v"(c3) : "v"(a));             \
+      asm volatile(ASM : "+v"(c4) : "v"(a)); asm volatile(ASM : "+v"(c5) : "v"(a));             \
+      asm volatile(ASM : "+v"(c6) : "v"(a)); asm volatile(ASM : "+v"(c7) : "v"(a));             \
+    }                                                                                           \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7); \
+  }
+#define I32(k) (uint32_t)(seed + threadIdx.x + k)
+#define I64(k) (uint64_t)(seed + threadIdx.x + k)
+SIMPLE_KERNEL(k_add_u32, "v_add_u32 %0, %0, %1", uint32_t, I32)
+SIMPLE_KERNEL(k_and_b32, "v_and_b32 %0, %0, %1", uint32_t, I32)
+SIMPLE_KERNEL(k_mov_b32, "v_mov_b32 %0, %1", uint32_t, I32)
+SIMPLE_KERNEL(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1", uint64_t, I64)
+SIMPLE_KERNEL(k_lshrrev_b64, "v_lshrrev_b64 %0, 3, %0", uint64_t, I64)
+SIMPLE_KERNEL(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc", uint32_t, I32)
+__global__ void k_add_f32(uint64_t* out, uint32_t seed) {
+  float a = 1.0f + threadIdx.x;
+  float c0 = a, c1 = a + 1, c2 = a + 2, c3 = a + 3, c4 = a + 4, c5 = a + 5, c6 = a + 6, c7 = a + 7;
+  for (int i = 0; i < ITERS; ++i) {
+#define ADDF(c) asm volatile("v_add_f32 %0, %0, %1" : "+v"(c) : "v"(a));
+    ADDF(c0) ADDF(c1) ADDF(c2) ADDF(c3) ADDF(c4) ADDF(c5) ADDF(c6) ADDF(c7)
+#undef ADDF
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7);
+}
+// accumulator-register round trip (the spill slots of a 512-register kernel)
+__global__ void k_accvgpr(uint64_t* out, uint32_t seed) {
+  uint32_t c0 = seed + threadIdx.x, c1 = c0 + 1, c2 = c0 + 2, c3 = c0 + 3;
+  for (int i = 0; i < ITERS; ++i) {
+#define ACC(c, r) asm volatile("v_accvgpr_write_b32 " r ", %0\n v_accvgpr_read_b32 %0, " r : "+v"(c) :: r);
+    ACC(c0, "a0") ACC(c1, "a1") ACC(c2, "a2") ACC(c3, "a3")
+#undef ACC
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(c0 ^ c1 ^ c2 ^ c3);
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 static int bench(const char* name, kfn k, uint64_t* d, int blocks, int threads, double* rate_out) {
@@ -136,6 +181,21 @@ int main() {
   bench("v_fma_f64", k_fma_f64, d, blocks, threads, &r);
   // one wave per SIMD (the occupancy a 512-VGPR kernel gets)
   bench("v_mad_u64_u32@1wave/SIMD", k_mad_u64_u32, d, cus, threads, &r);
+  // 8 waves per SIMD vs one wave per SIMD for the simple ops
+  const struct { const char* n; kfn k; } simple[] = {
+      {"v_add_u32", k_add_u32}, {"v_and_b32", k_and_b32}, {"v_mov_b32", k_mov_b32},
+      {"v_lshl_add_u64", k_lshl_add_u64}, {"v_lshrrev_b64", k_lshrrev_b64}, {"v_cndmask_b32", k_cndmask},
+      {"v_add_f32", k_add_f32}, {"v_accvgpr_write+read(2 instr)", k_accvgpr}};
+  for (const auto& s : simple) {
+    char nm[96];
+    snprintf(nm, sizeof nm, "%s@8waves/SIMD", s.n);
+    bench(nm, s.k, d, blocks, threads, &r);
+    snprintf(nm, sizeof nm, "%s@2waves/SIMD", s.n);
+    bench(nm, s.k, d, cus * 2, threads, &r);
+    snprintf(nm, sizeof nm, "%s@1wave/SIMD", s.n);
+    bench(nm, s.k, d, cus, threads, &r);
+  }
+  bench("v_mad_u64_u32@2waves/SIMD", k_mad_u64_u32, d, cus * 2, threads, &r);
   CHECK(hipFree(d));
   return 0;
 }
