@@ -160,6 +160,23 @@ int bgv_hash_to_g2(bgv_ctx* ctx, const uint8_t* msgs, const uint32_t* lens, size
 int bgv_verify_partial(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, uint8_t out576[576], int32_t out_codes[2]);
 int bgv_final_verify(bgv_ctx* ctx, const uint8_t* partials, size_t n, int32_t* out_verdict);
 
+/* Parity hook (tests only): the per-set intermediates of a verify call's kernels with the
+ * path forced, so the latency path (which serves every call of up to 16,384 pairs: gossip,
+ * block import) is checked byte for byte against the bulk path and the hash_to_G2 goldens.
+ *   path 1 (BGV_PATH_BULK)     k_prep (task_hash/task_sig/task_pk), k_miller one pair per lane
+ *   path 2 (BGV_PATH_LATENCY)  k_prep_a + k_prep_team, k_miller_team
+ * The n sets (cached pubkeys only) form one job in groups of 64; set i gets the i-th nonzero
+ * splitmix64 output from `seed` as its randomizer, so both paths see the same r_i.
+ *   out_h192[i]    H(m_i), serialized like bgv_hash_to_g2
+ *   out_f576[i]    its Miller-loop value f_i = e(r_i pk_i, H(m_i)) before the final
+ *                  exponentiation (12 canonical big-endian Fp coefficients, tower order; 1 when
+ *                  the set takes no part)
+ *   out_status[2i], [2i+1]  the set's signature / pubkey status (0, 100 = infinity, or BLST code) */
+#define BGV_PATH_BULK 1
+#define BGV_PATH_LATENCY 2
+int bgv_debug_prepare(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, int path, uint64_t seed, uint8_t* out_h192,
+                      uint8_t* out_f576, int32_t* out_status);
+
 /* SURVEY 8(f) rows beside the verify path -------------------------------- */
 
 /* Deposit-time pubkey validation: bls.PublicKey.fromBytes(pubkey, CoordType.affine,

@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libblsgpu.so")
 # kernel translation units (compiled in parallel; each carries its own copy of the
 # out-of-line arithmetic with its own register budget) and the host orchestration
-KERNEL_UNITS = ["bgv_k_prep.hip", "bgv_k_miller.hip", "bgv_k_final.hip", "bgv_k_util.hip"]
+KERNEL_UNITS = ["bgv_k_prep_bulk.hip", "bgv_k_prep.hip", "bgv_k_miller.hip", "bgv_k_final.hip", "bgv_k_util.hip"]
 SOURCES = [os.path.join(CSRC, f) for f in KERNEL_UNITS] + [os.path.join(CSRC, "bgv_api.cpp")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("BGV_OFFLOAD_ARCH", "gfx950")
@@ -39,8 +39,8 @@ def _headers():
 
 
 def build(force=False, verbose=True, lib=LIB, defines=(), extra_flags=()):
-    """defines: extra -D flags, extra_flags: extra compiler flags (tuning variants built to
-    another `lib` path).  Objects are
+    """defines: extra -D flags, extra_flags: extra compiler flags (A/B builds to another `lib`
+    path: tools/ab_build.py; the product build takes neither).  Objects are
     cached per source under build/obj (the kernel unit takes minutes; the host unit seconds)
     and rebuilt when the source or any header is newer."""
     if not force and up_to_date(lib):
@@ -100,11 +100,5 @@ def build_node(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    if "--variant" in sys.argv:  # --variant NAME DEF1 [DEF2 ...]: lodestar_amd/libblsgpu_NAME.so
-        i = sys.argv.index("--variant")    # (BGV_VARIANT_FLAGS env: extra compiler flags)
-        name, defs = sys.argv[i + 1], sys.argv[i + 2:]
-        flags = os.environ.get("BGV_VARIANT_FLAGS", "").split()
-        print(build(force=True, lib=os.path.join(HERE, "libblsgpu_%s.so" % name), defines=defs, extra_flags=flags))
-        sys.exit(0)
     build(force="--force" in sys.argv)
     build_node(force="--force" in sys.argv)

@@ -153,8 +153,20 @@ struct Exec {
   size_t pout_cap = 0;
 };
 
+// bgv_final_verify's device buffers (under util_mu)
+struct FinalScratch {
+  uint8_t* din = nullptr;
+  void* vals = nullptr;
+  void* one = nullptr;
+  bgv_dgroup* dg = nullptr;
+  int32_t* dst = nullptr;
+  int32_t* dv = nullptr;
+  size_t cap = 0;
+};
+
 struct Device {
   int id = 0;
+  FinalScratch final_scratch;
   hipStream_t stream = nullptr;      // utility work (cache upload, hooks, keygen)
   bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
   size_t cache_cap = 0;
@@ -941,6 +953,13 @@ static void ctx_free_devices(bgv_ctx* c) {
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
+    {
+      FinalScratch& fs = d.final_scratch;
+      void* bufs[] = {fs.din, fs.vals, fs.one, fs.dg, fs.dst, fs.dv};
+      for (void* q : bufs)
+        if (q) (void)hipFree(q);
+      fs = FinalScratch{};
+    }
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.stream = nullptr;
   }
@@ -1147,30 +1166,123 @@ int bgv_final_verify(bgv_ctx* c, const uint8_t* partials, size_t n, int32_t* out
   std::vector<uint8_t> in(576 * m);
   if (n) memcpy(in.data(), partials, 576 * n);
   else fp12_one_bytes(in.data());
-  uint8_t* din = nullptr;
-  void *vals = nullptr, *one = nullptr;
-  bgv_dgroup* dg = nullptr;
-  int32_t *dst = nullptr, *dv = nullptr;
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&din), 576 * m));
-  HIPCHK(hipMalloc(&vals, bgv_fp12_bytes() * m));
-  HIPCHK(hipMalloc(&one, bgv_fp12_bytes()));
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dg), sizeof(bgv_dgroup)));
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dst), 4 * m));
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dv), 4));
+  // persistent buffers, grown to the largest n seen (a hipFree would synchronize the device
+  // against the super-batches running on it)
+  FinalScratch& fs = d.final_scratch;
+  if (m > fs.cap) {
+    void* bufs[] = {fs.din, fs.vals, fs.one, fs.dg, fs.dst, fs.dv};
+    for (void* q : bufs)
+      if (q) (void)hipFree(q);
+    fs = FinalScratch{};
+    const size_t cap = std::max<size_t>(m, 8);
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&fs.din), 576 * cap));
+    HIPCHK(hipMalloc(&fs.vals, bgv_fp12_bytes() * cap));
+    HIPCHK(hipMalloc(&fs.one, bgv_fp12_bytes()));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&fs.dg), sizeof(bgv_dgroup)));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&fs.dst), 4 * cap));
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&fs.dv), 4));
+    fs.cap = cap;
+  }
   const bgv_dgroup g{0, (uint32_t)m};
-  HIPCHK(hipMemcpyAsync(din, in.data(), 576 * m, hipMemcpyHostToDevice, d.stream));
-  HIPCHK(hipMemcpyAsync(dg, &g, sizeof(g), hipMemcpyHostToDevice, d.stream));
-  HIPCHK(bgv_launch_final_verify(din, (uint32_t)m, vals, one, dg, dst, dv, d.stream));
+  HIPCHK(hipMemcpyAsync(fs.din, in.data(), 576 * m, hipMemcpyHostToDevice, d.stream));
+  HIPCHK(hipMemcpyAsync(fs.dg, &g, sizeof(g), hipMemcpyHostToDevice, d.stream));
+  HIPCHK(bgv_launch_final_verify(fs.din, (uint32_t)m, fs.vals, fs.one, fs.dg, fs.dst, fs.dv, d.stream));
   std::vector<int32_t> st(m);
   int32_t v = 0;
-  HIPCHK(hipMemcpyAsync(st.data(), dst, 4 * m, hipMemcpyDeviceToHost, d.stream));
-  HIPCHK(hipMemcpyAsync(&v, dv, 4, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(st.data(), fs.dst, 4 * m, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(&v, fs.dv, 4, hipMemcpyDeviceToHost, d.stream));
   HIPCHK(hipStreamSynchronize(d.stream));
-  void* bufs[] = {din, vals, one, dg, dst, dv};
-  for (void* q : bufs) (void)hipFree(q);
   for (int32_t x : st)
     if (x) return -BGV_E_ARG;  // a coefficient >= p: not a serialized partial
   *out_verdict = v;
+  return BGV_OK;
+}
+
+int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, uint64_t seed, uint8_t* out_h192,
+                      uint8_t* out_f576, int32_t* out_status) {
+  if (!c || (nsets && (!sets || !out_h192 || !out_f576 || !out_status)) ||
+      (path != BGV_PATH_BULK && path != BGV_PATH_LATENCY))
+    return -BGV_E_ARG;
+  if (nsets == 0) return BGV_OK;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
+  // one job's layout: groups of 64 consecutive slots, every slot hashes its own root
+  std::vector<bgv_dslot> slots;
+  std::vector<bgv_dgroup> groups;
+  std::vector<uint32_t> idx;
+  uint64_t state = seed;
+  uint32_t max_npk = 0;
+  for (size_t i = 0; i < nsets; ++i) {
+    const bgv_set& st = sets[i];
+    if (!st.pk_indices || st.n_pk == 0 || !st.msg || (st.sig_len && !st.sig)) return -BGV_E_ARG;
+    for (uint32_t q = 0; q < st.n_pk; ++q)
+      if (st.pk_indices[q] >= c->n_pubkeys) return -BGV_E_BAD_INDEX;
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.flags = BGV_SLOT_PK_CACHED;
+    s.n_pk = st.n_pk;
+    s.sig_len = st.sig_len;
+    s.pk_off = (uint32_t)idx.size();
+    idx.insert(idx.end(), st.pk_indices, st.pk_indices + st.n_pk);
+    memcpy(s.msg, st.msg, 32);
+    if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
+    s.group = (uint32_t)(i / BGV_WAVE);
+    s.hsrc = (uint32_t)i;
+    do s.scalar = splitmix64(&state);
+    while (s.scalar == 0);
+    max_npk = std::max(max_npk, st.n_pk);
+    slots.push_back(s);
+  }
+  while (slots.size() % BGV_WAVE) {
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.flags = BGV_SLOT_PAD;
+    s.hsrc = (uint32_t)slots.size();
+    slots.push_back(s);
+  }
+  for (size_t g = 0; g * BGV_WAVE < nsets; ++g)
+    groups.push_back(bgv_dgroup{(uint32_t)(g * BGV_WAVE), (uint32_t)std::min<size_t>(BGV_WAVE, nsets - g * BGV_WAVE)});
+  const uint32_t nslots = (uint32_t)slots.size(), ngroups = (uint32_t)groups.size();
+  std::lock_guard<std::mutex> lk(c->util_mu);
+  Device& d = c->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  Exec* x = new Exec();
+  uint8_t *dh = nullptr, *df = nullptr;
+  int rc = exec_create(x);
+  if (!rc) rc = exec_reserve_slots(*x, nslots);
+  if (!rc) rc = exec_reserve_groups(*x, ngroups);
+  if (!rc) rc = grow(&x->d_idx, &x->idx_cap, idx.size());
+  if (!rc && (hipMalloc(reinterpret_cast<void**>(&dh), 192ull * nslots) != hipSuccess ||
+              hipMalloc(reinterpret_cast<void**>(&df), 576ull * nslots) != hipSuccess))
+    rc = -BGV_E_DEVICE;
+  std::vector<int32_t> ss(nslots), ps(nslots);
+  if (!rc) {
+    bgv_dev_batch b = make_batch(d, *x, nslots, ngroups);
+    b.max_npk = max_npk;
+    b.path = path;
+    bgv_streams S{x->main, nullptr};
+    const bool ok =
+        hipMemcpyAsync(x->d_slots, slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x->main) ==
+            hipSuccess &&
+        hipMemcpyAsync(x->d_groups, groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x->main) ==
+            hipSuccess &&
+        hipMemcpyAsync(x->d_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, x->main) == hipSuccess &&
+        bgv_launch_sets(b, S) == hipSuccess && bgv_launch_debug_out(b, dh, df, x->main) == hipSuccess &&
+        hipMemcpyAsync(out_h192, dh, 192 * nsets, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+        hipMemcpyAsync(out_f576, df, 576 * nsets, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+        hipMemcpyAsync(ss.data(), b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+        hipMemcpyAsync(ps.data(), b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+        hipStreamSynchronize(x->main) == hipSuccess;
+    if (!ok) rc = -BGV_E_DEVICE;
+  }
+  if (dh) (void)hipFree(dh);
+  if (df) (void)hipFree(df);
+  exec_destroy(x);
+  if (rc) return rc;
+  for (size_t i = 0; i < nsets; ++i) {
+    out_status[2 * i] = ss[i];
+    out_status[2 * i + 1] = ps[i];
+  }
   return BGV_OK;
 }
 

@@ -68,23 +68,20 @@ __device__ __forceinline__ bool slot_live(const bgv_dslot& d, int32_t ss, int32_
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 
 // Latency path (small calls): at most this many pairs (sets + groups) take the split
-// k_prep_a / k_prep_b and the team Miller loop instead of one lane per set and task, which
+// k_prep_a / k_prep_team and the team Miller loop instead of one lane per set and task, which
 // wins while the chip would otherwise sit mostly idle (one lane per set runs ~13 ms in
 // k_miller however small the call).  BGV_LATENCY_MAX overrides (0 disables).
-// group closing on 12-lane teams (k_final12) instead of 16 (BGV_FINAL12=0: k_final)
-static inline bool bgv_final12() {
-  static const bool v = [] {
-    const char* e = getenv("BGV_FINAL12");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
 static inline uint32_t bgv_latency_max() {
   static const uint32_t v = [] {
     const char* e = getenv("BGV_LATENCY_MAX");
     return e ? (uint32_t)strtoul(e, nullptr, 10) : 16384u;
   }();
   return v;
+}
+
+// the latency path's kernels for this batch: forced by b.path, else by size
+static inline bool bgv_use_latency(const bgv_dev_batch& b, uint32_t pairs) {
+  return b.path == BGV_PATH_LATENCY || (b.path == BGV_PATH_AUTO && pairs <= bgv_latency_max());
 }
 
 // Kernel k of a verify launch is bracketed by events kev[2k], kev[2k+1] when profiling.

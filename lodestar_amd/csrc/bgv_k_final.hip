@@ -188,12 +188,9 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod);
-  else if (bgv_final12())
+  else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod);
-  else
-    hipLaunchKernelGGL(k_final, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
-                       b.f, b.gpair, b.verdict, b.gprod);
   BGV_MARK(5);
   return hipGetLastError();
 }

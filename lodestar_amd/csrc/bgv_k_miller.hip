@@ -163,9 +163,6 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
 
 }  // extern "C"
 
-#ifndef BGV_ROUND_SPLIT
-#define BGV_ROUND_SPLIT 1
-#endif
 // lanes of one k_miller round: one wave of 64 on each SIMD (MI355X: 256 CUs x 4 SIMDs)
 static uint32_t miller_round_lanes() {
   static const uint32_t lanes = [] {
@@ -186,10 +183,11 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
                      b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
   BGV_MARK(2);
   const uint32_t R = miller_round_lanes();
-  if (n + b.ngroups <= bgv_latency_max()) {
+  if (bgv_use_latency(b, n + b.ngroups)) {
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(n + b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, n,
                        b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
-  } else if (BGV_ROUND_SPLIT && b.ngroups <= bgv_latency_max() && (n + b.ngroups + R - 1) / R > (n + R - 1) / R) {
+  } else if (b.path != BGV_PATH_BULK && b.ngroups <= bgv_latency_max() &&
+             (n + b.ngroups + R - 1) / R > (n + R - 1) / R) {
     // the group pairs on extra k_miller lanes would open one more round of one wave per SIMD
     // (131,072 sets + 2,048 groups: 3 rounds instead of 2); run them on teams instead
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, 0u,

@@ -1,20 +1,17 @@
-// Per-set preparation kernels (gfx950): k_pk_agg and k_prep (see bgv_api.cpp for the
-// launch order of a verify call and bgv_k_miller.hip / bgv_k_final.hip for the rest).
+// Per-set preparation kernels (gfx950) other than the bulk k_prep (bgv_k_prep_bulk.hip);
+// see bgv_api.cpp for the launch order of a verify call and bgv_k_miller.hip /
+// bgv_k_final.hip for the rest.
 //
 //   k_pk_agg16 / k_pk_agg  (only when a call holds a set with >= BGV_PK_TREE_MIN cached
 //              keys) a team of 16 lanes per committee-sized set, a whole wavefront per set
 //              above BGV_PK_TEAM_MAX keys, sums its keys with a ds_swizzle/ds_bpermute tree
-//   k_prep_a / k_prep_b   the latency path for small calls (bgv_latency_max): the same
-//              work over two launches with twice the lanes per set, so the longest chain
-//              per lane roughly halves: (a) one SSWU map + isogeny per lane for u0 and u1,
-//              the signature's decompression, the pubkey task; (b) the cofactor clearing of
-//              q0 + q1, and the signature's subgroup check beside r_i * sig_i
-//   k_prep     three independent tasks side by side (blockIdx.y):
-//              sig  decompress + subgroup-check the 96-byte signature, then r_i * sig_i
-//                   (Jacobian G2, summed per group by k_gsum)
-//              hash hash_to_G2(signing root) -> H(m_i), Jacobian
-//              pk   gather + aggregate pubkeys from the device cache; r_i * pk_i (Jacobian)
-#include "bgv_device.h"
+//   k_prep_a / k_prep_team   the latency path for small calls (bgv_latency_max): the same
+//              work over two launches with more lanes per set, so the longest chain per
+//              lane roughly halves: (a) one SSWU map + isogeny per lane for u0 and u1, the
+//              signature's decompression, the pubkey task; (team) the cofactor clearing of
+//              q0 + q1 and r_i * sig_i on 16-lane teams, the subgroup check on one lane
+//   k_prep     (bgv_k_prep_bulk.hip) sig, hash and pk tasks side by side for larger calls
+#include "bgv_k_tasks.h"
 #include "bgv_team_dev.h"
 #include "bgv_tcurve.h"
 
@@ -59,98 +56,6 @@ struct tc_dev_engine {
 
 extern "C" {
 
-
-// r_i * sig_i of a set whose signature decodes and lies in G2 (else only a status).
-__device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
-                                      int32_t* __restrict__ sig_status) {
-  const bgv_dslot& d = slots[s];
-  int32_t st = BGV_ST_OK;
-  if (d.flags & BGV_SLOT_PAD) {
-    st = BGV_ST_INFINITY;
-  } else if (d.sig_len != 96) {
-    st = BGV_INVALID_SIZE;
-  } else {
-    uint8_t b[96];
-    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
-    g2_aff a;
-    bool inf;
-    st = g2_decompress(&a, &inf, b);
-    if (st == BGV_OK) {
-      if (inf) {
-        st = BGV_ST_INFINITY;  // skipped in the accumulator, as blst does
-      } else {
-        const g2_jac j = jac_from_aff(a);
-        if (!g2_in_subgroup(j))
-          st = BGV_POINT_NOT_IN_GROUP;
-        else
-          rsig[s] = jac_mul_u64(j, d.scalar);  // never infinity: 0 < r < group order
-      }
-    }
-  }
-  sig_status[s] = st;
-}
-
-__device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
-  const bgv_dslot& d = slots[s];
-  if (d.flags & BGV_SLOT_PAD) return;
-  uint8_t msg[32];
-  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
-  h[s] = hash_to_g2(msg, 32);  // stays Jacobian: k_miller adds it with miller_add_jq
-}
-
-// Sum of one set's pubkeys (PublicKey.aggregate, chain/bls/utils.ts:5-16): the k_pk_agg
-// tree sum when the set went through it, else serial mixed additions of cached keys or of
-// 96-byte records (decoded like blst's PublicKey.fromBytes, bls_curve.h g1_deserialize).
-// *st receives the first record's decode error, if any.
-__device__ __noinline__ static g1_jac pk_sum(const bgv_dslot& d, const uint32_t* __restrict__ pk_idx,
-                                      const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
-                                      const g1_jac* __restrict__ pk_agg, uint32_t s, int32_t* st) {
-  g1_jac acc = jac_infinity<fp_t>();
-  const bool cached = (d.flags & BGV_SLOT_PK_CACHED) != 0;
-  const bool tree = pk_agg != nullptr && cached && d.n_pk >= BGV_PK_TREE_MIN;  // summed by k_pk_agg
-  if (tree) return pk_agg[s];
-  for (uint32_t k = 0; k < d.n_pk; ++k) {
-    g1_aff a;
-    if (cached) {
-      a = cache[pk_idx[d.pk_off + k]];
-    } else {
-      uint8_t b[96];
-      const uint8_t* src = pk_bytes + 96ull * (d.pk_off + k);
-      for (int i = 0; i < 96; ++i) b[i] = src[i];
-      bool inf;
-      const int rc = g1_deserialize(&a, &inf, b);
-      if (rc != BGV_OK) {
-        *st = rc;
-        break;
-      }
-      if (inf) continue;
-    }
-    acc = jac_add_aff(acc, a);
-  }
-  return acc;
-}
-
-__device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
-                                     const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                     const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                     int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
-  const bgv_dslot& d = slots[s];
-  int32_t st = BGV_ST_OK;
-  if (d.flags & BGV_SLOT_PAD) {
-    pk_status[s] = BGV_ST_INFINITY;
-    return;
-  }
-  const g1_jac acc = pk_sum(d, pk_idx, cache, pk_bytes, pk_agg, s, &st);
-  if (st == BGV_OK) {
-    // Jacobian: the Miller loop takes P projectively (bls_pairing.h miller_p), no inversion
-    const g1_jac rp = jac_mul_u64(acc, d.scalar);
-    if (jac_is_inf(rp))
-      st = BGV_ST_INFINITY;  // infinity aggregate: BLST_PK_IS_INFINITY / false (job_precheck)
-    else
-      rpk[s] = rp;
-  }
-  pk_status[s] = st;
-}
 
 // Pubkey aggregation of many-key sets as a wavefront tree (one wave per slot): lane l
 // sums the set's cached keys l, l + 64, ... with mixed additions (coalesced gathers),
@@ -240,27 +145,6 @@ __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uin
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
 }
 
-__global__ void BGV_KATTR_PREP k_prep_b(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
-                                        fp12_t* __restrict__ f, g2_jac* __restrict__ rsig,
-                                        int32_t* __restrict__ sig_status) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nslots) return;
-  const bgv_dslot& d = slots[s];
-  if (d.flags & BGV_SLOT_PAD) return;
-  if (blockIdx.y == 0) {
-    h[s] = g2_clear_cofactor(jac_add(h[s], *split_q1(f, s)));
-    return;
-  }
-  // the decode status is final unless it is OK (then only the subgroup lane may change it)
-  if (sig_status[s] != BGV_ST_OK) return;
-  const g2_jac j = jac_from_aff(*split_sig(f, s));
-  if (blockIdx.y == 1) {
-    if (!g2_in_subgroup(j)) sig_status[s] = BGV_POINT_NOT_IN_GROUP;
-  } else {
-    rsig[s] = jac_mul_u64(j, d.scalar);  // unused unless the subgroup lane leaves the status OK
-  }
-}
-
 // The latency path's second launch on teams (bgv_tcurve.h): blockIdx.y = 0 the cofactor
 // clearing of q0 + q1 (one team per set), 1 r_i * sig_i (one team per set), 2 the
 // signature's subgroup check (one lane per set).  A team whose cofactor clearing met an
@@ -319,7 +203,7 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
     else if (c < 6)
       S[TCP_BANK(1) + c] = c == 4 ? fp_one() : fp_zero();
     __syncthreads();
-    tc_mul_u64(e, d.scalar);
+    tc_mul_glv(e, d.scalar);
     if (real && ok && c < 6) reinterpret_cast<fp_t*>(rsig + uu)[c] = S[TCP_BANK(4) + c];
   }
 }
@@ -363,32 +247,6 @@ k_pk_agg16(const bgv_dslot* __restrict__ slots, uint32_t nslots, const uint32_t*
   if (act && l == 0) pk_agg[s] = acc;
 }
 
-// The three independent per-set tasks in one launch (blockIdx.y = task), so one
-// batch keeps 3x the wavefronts in flight on a single stream.
-__global__ void BGV_KATTR_PREP k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
-                                      int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
-                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                      const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg,
-                                      const uint32_t* __restrict__ uniq, uint32_t nuniq) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  // hash first: the longest task starts earliest.  With uniq, lane u hashes the u-th distinct
-  // signing root (slot uniq[u]); lanes past nuniq -- whole waves of them -- exit at once.
-  if (blockIdx.y == 0) {
-    if (uniq) {
-      if (s < nuniq) task_hash(uniq[s], slots, h);
-    } else if (s < nslots) {
-      task_hash(s, slots, h);
-    }
-    return;
-  }
-  if (s >= nslots) return;
-  if (blockIdx.y == 1)
-    task_sig(s, slots, rsig, sig_status);
-  else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
-}
-
 // PublicKey.aggregate(...).toBytes(uncompressed) over cached keys through the verify
 // path's own code: pk_sum of one slot (k_pk_agg's tree sum for >= BGV_PK_TREE_MIN keys,
 // task_pk's serial sum below), then affine and the 96-byte ZCash encoding.
@@ -419,16 +277,15 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   if (b.max_npk > BGV_PK_TEAM_MAX)
     hipLaunchKernelGGL(k_pk_agg, dim3(n), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
                        reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
-  if (n + b.ngroups <= bgv_latency_max()) {
+  if (bgv_use_latency(b, n + b.ngroups)) {
     hipLaunchKernelGGL(k_prep_a, dim3(nblk(n, 64), 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
                        tree ? b.pk_agg : nullptr);
     hipLaunchKernelGGL(k_prep_team, dim3(nblk(n, BGV_FINAL_TEAMS), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f,
                        b.rsig, b.sig_status);
   } else {
-    hipLaunchKernelGGL(k_prep, dim3(nblk(n, 64), 3), dim3(64), 0, s.main, b.slots, n, b.rsig, b.sig_status, b.h,
-                       b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                       tree ? b.pk_agg : nullptr, b.uniq, b.nuniq);
+    const hipError_t e = bgv_launch_prep_bulk(b, s, tree);
+    if (e != hipSuccess) return e;
   }
   BGV_MARK(1);
   return hipGetLastError();

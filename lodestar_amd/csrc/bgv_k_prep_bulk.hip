@@ -1,0 +1,50 @@
+// The bulk preparation kernel of a verify call (gfx950), in a unit of its own so that its
+// register budget (BGV_WPE_PREP waves per SIMD) applies to every function it calls: a
+// device function shared with a kernel of another budget is compiled for the larger one.
+//
+//   k_prep  three independent tasks side by side (blockIdx.y): hash (H(m_i)), sig (decode,
+//           subgroup check, r_i * sig_i) and pk (aggregate, r_i * pk_i); see bgv_k_tasks.h
+#include "bgv_k_tasks.h"
+
+// waves per SIMD the bulk k_prep is register-budgeted for (1: 512 registers, 2: 256)
+#ifndef BGV_WPE_BULK
+#define BGV_WPE_BULK 1
+#endif
+#define BGV_KATTR_BULK __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_BULK, BGV_WPE_BULK)))
+
+extern "C" {
+
+// The three independent per-set tasks in one launch (blockIdx.y = task), so one
+// batch keeps 3x the wavefronts in flight on a single stream.
+__global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
+                                      int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
+                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                      const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
+                                      int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg,
+                                      const uint32_t* __restrict__ uniq, uint32_t nuniq) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  // hash first: the longest task starts earliest.  With uniq, lane u hashes the u-th distinct
+  // signing root (slot uniq[u]); lanes past nuniq -- whole waves of them -- exit at once.
+  if (blockIdx.y == 0) {
+    if (uniq) {
+      if (s < nuniq) task_hash(uniq[s], slots, h);
+    } else if (s < nslots) {
+      task_hash(s, slots, h);
+    }
+    return;
+  }
+  if (s >= nslots) return;
+  if (blockIdx.y == 1)
+    task_sig(s, slots, rsig, sig_status);
+  else
+    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+}
+
+}  // extern "C"
+
+hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree) {
+  hipLaunchKernelGGL(k_prep, dim3(nblk(b.nslots, 64), 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig, b.sig_status,
+                     b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
+                     tree ? b.pk_agg : nullptr, b.uniq, b.nuniq);
+  return hipGetLastError();
+}

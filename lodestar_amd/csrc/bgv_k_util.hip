@@ -101,6 +101,26 @@ __global__ void k_hash_msgs(const uint8_t* __restrict__ msgs, const uint32_t* __
   for (int k = 0; k < 192; ++k) out192[192ull * i + k] = b[k];
 }
 
+// Parity hook (bgv_debug_prepare): per slot, its H(m) serialized like k_hash_msgs and its
+// Miller-loop value f as 12 canonical big-endian Fp coefficients (k_fp12_to_bytes order)
+__global__ void k_debug_out(const bgv_dslot* __restrict__ slots, uint32_t n, const g2_jac* __restrict__ h,
+                            const fp12_t* __restrict__ f, uint8_t* __restrict__ out_h192,
+                            uint8_t* __restrict__ out_f576) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  g2_aff a;
+  const bool fin = jac_to_aff(&a, h[slots[s].hsrc]);
+  uint8_t b[192];
+  g2_serialize(b, a, !fin);
+  for (int k = 0; k < 192; ++k) out_h192[192ull * s + k] = b[k];
+  const fp_t* v = reinterpret_cast<const fp_t*>(f + s);
+  for (int i = 0; i < 12; ++i) {
+    uint8_t c[48];
+    fp_to_be48(c, fp_from_mont(v[i]));
+    for (int k = 0; k < 48; ++k) out_f576[576ull * s + 48 * i + k] = c[k];
+  }
+}
+
 // 48-byte compressed pubkeys -> device cache entries (trusted, no subgroup check:
 // state-transition/src/cache/pubkeyCache.ts:75 decompresses without validation)
 __global__ void k_cache_put_compressed(const uint8_t* __restrict__ keys, uint32_t n, g1_aff* __restrict__ cache,
@@ -216,6 +236,12 @@ hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_ca
     hipLaunchKernelGGL(k_cache_put_compressed, dim3(nblk(n, 64)), dim3(64), 0, st, keys, n, c, status);
   else
     hipLaunchKernelGGL(k_cache_put_uncompressed, dim3(nblk(n, 64)), dim3(64), 0, st, keys, n, c, status);
+  return hipGetLastError();
+}
+
+hipError_t bgv_launch_debug_out(const bgv_dev_batch& b, uint8_t* out_h192, uint8_t* out_f576, hipStream_t st) {
+  hipLaunchKernelGGL(k_debug_out, dim3(nblk(b.nslots, 64)), dim3(64), 0, st, b.slots, b.nslots, b.h, b.f, out_h192,
+                     out_f576);
   return hipGetLastError();
 }
 

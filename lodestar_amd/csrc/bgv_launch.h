@@ -18,9 +18,17 @@ struct fp2_t;
 // opaque cache entry (affine G1, Montgomery form)
 struct bgv_cache_entry;
 
+// kernel path of a batch (the public values are in include/blsgpu.h)
+#define BGV_PATH_AUTO 0
+#ifndef BGV_PATH_BULK
+#define BGV_PATH_BULK 1
+#define BGV_PATH_LATENCY 2
+#endif
+
 struct bgv_dev_batch {
   uint32_t nslots, ngroups;
   uint32_t max_npk;  // largest n_pk of any slot (k_pk_agg runs only when a set reaches BGV_PK_TREE_MIN)
+  int path;          // BGV_PATH_AUTO by size, BGV_PATH_BULK / BGV_PATH_LATENCY forced (bgv_debug_prepare)
   // slots whose H(msg) the bulk k_prep computes (the first slot of each distinct signing root of
   // a call); the other slots read H at their hsrc.  Null: every slot hashes its own message.
   const uint32_t* uniq;
@@ -57,6 +65,7 @@ struct bgv_streams {
 };
 hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // prep + miller
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
+hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree);  // bgv_k_prep_bulk.hip
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
@@ -69,6 +78,7 @@ hipError_t bgv_launch_cache_put(const uint8_t* keys, uint32_t n, int fmt, bgv_ca
 hipError_t bgv_launch_aggregate(const bgv_dslot* slot, const uint32_t* idx, uint32_t n, const bgv_cache_entry* cache,
                                 void* agg, uint8_t* out96, hipStream_t st);
 size_t bgv_g1_point_bytes();
+hipError_t bgv_launch_debug_out(const bgv_dev_batch& b, uint8_t* out_h192, uint8_t* out_f576, hipStream_t st);
 hipError_t bgv_launch_hash(const uint8_t* msgs, const uint32_t* offs, const uint32_t* lens, uint32_t n,
                            uint8_t* out192, hipStream_t st);
 hipError_t bgv_launch_keygen(const uint8_t* sks, uint32_t n, bgv_cache_entry* cache, uint8_t* out48, hipStream_t st);

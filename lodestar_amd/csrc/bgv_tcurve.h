@@ -4,7 +4,7 @@
 //
 // A doubling is 3 rounds and an addition 5, against ~16 and ~43 chained products on one
 // lane, so the two 64-bit [x]-chains of the cofactor clearing and the 2-bit-window r * sig
-// finish ~2x sooner on an otherwise idle chip.  The schedules below restate bls_curve.h
+// (tc_mul_glv) finish ~2x sooner on an otherwise idle chip.  The schedules below restate bls_curve.h
 // step by step (g2_clear_cofactor, jac_mul_u64) over point "banks" of six LDS slots; the
 // engine E supplies the program runs and the bank moves, so the same schedule runs on the
 // device (bgv_k_prep.hip) and in the host emulation (tests/native/hostsim.cpp).
@@ -114,6 +114,49 @@ BGV_HD void tc_mul_u64(E& e, uint64_t k) {
   }
 }
 
+// r P for the randomizer r = lo32(k) + hi32(k) x^2 (bls_curve.h jac_mul_glv) with 2-bit
+// windows: P in bank 1 on entry, the result in bank 4.  Tables: P, 2P, 3P in banks 1-3 and
+// psi^2 of them (= [x^2] times, P in G2) in banks 6-8.  Per window: two doublings, then the
+// a-digit's and the b-digit's entries added through bank 0 (the per-team digit picks the
+// source bank), the accumulator taking the entry itself while it is still at infinity.
+// Both halves' prefixes are < 2^32 < x^2, so the accumulator never equals an entry or its
+// negative once it is finite: the generic addition programs are exact here.
+template <class E>
+BGV_HD void tc_mul_glv(E& e, uint64_t k) {
+  const uint32_t a = (uint32_t)k, b = (uint32_t)(k >> 32);
+  e.copy(0, 1);  // P
+  e.copy(4, 1);
+  e.run(TCP_DBL45);
+  e.copy(2, 5);       // 2P
+  e.run(TCP_ADD123);  // 3P
+  e.copy(9, 2);
+  e.run(TCP_PSI2_12);  // bank 1 still P
+  e.copy(6, 2);
+  e.copy(1, 9);
+  e.run(TCP_PSI2_12);
+  e.copy(7, 2);
+  e.copy(1, 3);
+  e.run(TCP_PSI2_12);
+  e.copy(8, 2);
+  e.copy(1, 0);
+  e.copy(2, 9);
+  bool inf = true;
+  for (int i = 30; i >= 0; i -= 2) {
+    e.run(TCP_DBL45);
+    e.run(TCP_DBL54);
+    const int da = (int)((a >> i) & 3u);
+    e.copy(0, da ? da : 1);
+    e.run(TCP_ADD405);
+    e.copy(4, da == 0 ? 4 : (inf ? 0 : 5));
+    inf = inf && da == 0;
+    const int db = (int)((b >> i) & 3u);
+    e.copy(0, db ? 5 + db : 6);
+    e.run(TCP_ADD405);
+    e.copy(4, db == 0 ? 4 : (inf ? 0 : 5));
+    inf = inf && db == 0;
+  }
+}
+
 #if !defined(__HIP_DEVICE_COMPILE__)
 // Host emulation engine (tests): programs lane by lane, bank moves as plain copies.
 struct tc_host_engine {
@@ -176,6 +219,15 @@ inline g2_jac tc_mul_u64_host(const g2_jac& p, uint64_t k) {
   tc_put(S, 1, p);
   tc_host_engine e{tab, S};
   tc_mul_u64(e, k);
+  return tc_get(S, 4);
+}
+inline g2_jac tc_mul_glv_host(const g2_jac& p, uint64_t k) {
+  static const uint8_t tab[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
+  static fp_t S[TCP_NSLOT];
+  tc_host_init(S);
+  tc_put(S, 1, p);
+  tc_host_engine e{tab, S};
+  tc_mul_glv(e, k);
   return tc_get(S, 4);
 }
 #endif

@@ -335,6 +335,46 @@ BGV_HD g2_jac g2_psi2(const g2_jac& p) {
   return r;
 }
 
+// The batch randomizers (bgv_dslot.scalar) are r = a + b x^2 mod the group order, a and b the
+// low and high 32 bits of the 64-bit word (never both zero).  x^2 is an eigenvalue of a cheap
+// endomorphism on both groups, so r P = a P + b E(P) costs 32 doublings instead of 64:
+//   G1  E(X, Y, Z) = (beta X, -Y, Z): phi(x, y) = (beta x, y) is [-x^2] on G1 for this beta
+//   G2  E = psi^2 = [p^2] = [x^2] on G2 (p = x mod the group order)
+// The 2^64 - 1 pairs (a, b) give distinct r (|a + b x^2| < 2^160 < the order), so a bad set
+// passes the batch equation with probability <= 2^-64, as with blst's 64-bit scalars.
+BGV_HD g1_jac jac_endo_x2(const g1_jac& p) {
+  const fp_t beta = {BGV_BETA_MX2};
+  return g1_jac{fp_mul(p.x, beta), fp_neg(p.y), p.z};
+}
+BGV_HD g2_jac jac_endo_x2(const g2_jac& p) { return g2_psi2(p); }
+
+// r P with r = lo32(k) + hi32(k) x^2: interleaved 3-bit fixed windows over one table
+// T[j] = jP (j < 8, in memory, one entry loaded per window and scalar half), the second
+// half's entry mapped through E on the fly; adds computed in every lane and selected, as in
+// jac_mul_u64.  Valid for P in the prime-order subgroup (a signature after its subgroup
+// check, a cached or aggregated pubkey); P infinity gives infinity.
+template <class F>
+BGV_NOINLINE jac_t<F> jac_mul_glv(const jac_t<F>& p, uint64_t k) {
+  constexpr int W = 3, NT = 1 << W, NWIN = (32 + W - 1) / W;
+  const uint32_t a = (uint32_t)k, b = (uint32_t)(k >> 32);
+  jac_t<F> tab[NT];
+  tab[1] = p;
+  tab[2] = jac_dbl(p);
+  BGV_NO_UNROLL for (int i = 3; i < NT; ++i) tab[i] = jac_add(tab[i - 1], p);
+  tab[0] = tab[1];
+  jac_t<F> acc = jac_infinity<F>();
+  BGV_NO_UNROLL for (int j = NWIN - 1; j >= 0; --j) {
+    BGV_UNROLL for (int t = 0; t < W; ++t) acc = jac_dbl(acc);
+    const uint32_t da = (a >> (W * j)) & (uint32_t)(NT - 1);
+    const jac_t<F> sa = jac_add(acc, tab[da]);
+    acc = jac_select(da != 0u, acc, sa);
+    const uint32_t db = (b >> (W * j)) & (uint32_t)(NT - 1);
+    const jac_t<F> sb = jac_add(acc, jac_endo_x2(tab[db]));
+    acc = jac_select(db != 0u, acc, sb);
+  }
+  return acc;
+}
+
 BGV_HD bool g2_aff_on_curve(const g2_aff& a) {
   const fp2_t b = BGV_B2;
   return fp2_eq(fp2_sqr(a.y), fp2_add(fp2_mul(fp2_sqr(a.x), a.x), b));

@@ -217,9 +217,7 @@ BGV_HD fp_t fp_neg(const fp_t& a) {
       uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11, uint32_t p##12, uint32_t p##13
 #define BGV_V14(x) x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11], x.v[12], x.v[13]
 
-BGV_MUL_ATTR fp_t fp_mul_l(BGV_U14(a_), BGV_U14(b_)) {
-  BGV_COUNT_MUL();
-  const fp_t a = {{BGV_L14(a_)}}, b = {{BGV_L14(b_)}};
+BGV_HD fp_t fp_mul_body(const fp_t& a, const fp_t& b) {
   const uint32_t P_[NL] = BGV_P_LIMBS;
   uint64_t t[NL];
   BGV_UNROLL for (int j = 0; j < NL; ++j) t[j] = 0;
@@ -241,10 +239,14 @@ BGV_MUL_ATTR fp_t fp_mul_l(BGV_U14(a_), BGV_U14(b_)) {
   return r;
 }
 
+BGV_MUL_ATTR fp_t fp_mul_l(BGV_U14(a_), BGV_U14(b_)) {
+  BGV_COUNT_MUL();
+  const fp_t a = {{BGV_L14(a_)}}, b = {{BGV_L14(b_)}};
+  return fp_mul_body(a, b);
+}
+
 // Montgomery square: 105 products (cross terms doubled) then 14 reduction rows.
-BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
-  BGV_COUNT_SQR();
-  const fp_t a = {{BGV_L14(a_)}};
+BGV_HD fp_t fp_sqr_body(const fp_t& a) {
   const uint32_t P_[NL] = BGV_P_LIMBS;
   uint64_t t[2 * NL];
   BGV_UNROLL for (int j = 0; j < 2 * NL; ++j) t[j] = 0;
@@ -265,6 +267,12 @@ BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
   }
   r.v[NL - 1] = (uint32_t)t[2 * NL - 1];
   return r;
+}
+
+BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
+  BGV_COUNT_SQR();
+  const fp_t a = {{BGV_L14(a_)}};
+  return fp_sqr_body(a);
 }
 
 BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_mul_l(BGV_V14(a), BGV_V14(b)); }

@@ -191,7 +191,12 @@ template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
 BGV_HD lzr lz_mul(const lz<LA, VA>& a, const lz<LB, VB>& b) {
   static_assert(LA * LB <= lzc::MUL_LIMB_MAX, "lz_mul: limb product overflows the column sums");
   static_assert(VA * VB <= lzc::VMUL_MAX, "lz_mul: operand values too large for a < 2p result");
+#if defined(BGV_LAZY_INLINE_MUL)
+  BGV_COUNT_MUL();
+  const fp_t r = fp_mul_body(fp_t{{BGV_V14(a)}}, fp_t{{BGV_V14(b)}});
+#else
   const fp_t r = fp_mul_l(BGV_V14(a), BGV_V14(b));
+#endif
   lzr o;
   BGV_UNROLL for (int i = 0; i < NL; ++i) o.v[i] = r.v[i];
   LZ_CHECK(o, "mul");
@@ -203,7 +208,12 @@ BGV_HD lzr lz_sqr(const lz<LA, VA>& a) {
   static_assert(LA < (1ull << 31), "lz_sqr: doubled limbs overflow 32 bits");
   static_assert(LA * LA <= lzc::MUL_LIMB_MAX, "lz_sqr: limb product overflows the column sums");
   static_assert(VA * VA <= lzc::VMUL_MAX, "lz_sqr: operand value too large for a < 2p result");
+#if defined(BGV_LAZY_INLINE_MUL)
+  BGV_COUNT_SQR();
+  const fp_t r = fp_sqr_body(fp_t{{BGV_V14(a)}});
+#else
   const fp_t r = fp_sqr_l(BGV_V14(a));
+#endif
   lzr o;
   BGV_UNROLL for (int i = 0; i < NL; ++i) o.v[i] = r.v[i];
   LZ_CHECK(o, "sqr");

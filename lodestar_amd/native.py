@@ -30,6 +30,8 @@ BGV_E_CLOSED = 32
 
 MODE_WORKER = 0
 MODE_PER_JOB = 1
+PATH_BULK = 1
+PATH_LATENCY = 2
 PK_COMPRESSED = 48
 PK_UNCOMPRESSED = 96
 
@@ -38,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "bgv_verify_async", "bgv_aggregate_pubkeys", "bgv_hash_to_g2", "bgv_keygen", "bgv_sign",
     "bgv_set_rng_seed", "bgv_strerror", "bgv_device_count", "bgv_profile",
     "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify", "bgv_set_batching",
-    "bgv_verify_partial", "bgv_final_verify",
+    "bgv_verify_partial", "bgv_final_verify", "bgv_debug_prepare",
 ]
 
 
@@ -103,6 +105,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_set_batching": ([P, U32, U32, U32], ctypes.c_int),
             "bgv_verify_partial": ([P, P, SZ, P, P], ctypes.c_int),
             "bgv_final_verify": ([P, P, SZ, P], ctypes.c_int),
+            "bgv_debug_prepare": ([P, P, SZ, ctypes.c_int, U64, P, P, P], ctypes.c_int),
             "bgv_strerror": ([ctypes.c_int], ctypes.c_char_p),
             "bgv_device_count": ([], ctypes.c_int),
             "bgv_profile": ([P, ctypes.c_int, P, P, ctypes.c_int, P], ctypes.c_int),
@@ -274,6 +277,18 @@ class Context:
         codes = (ctypes.c_int32 * 2)()
         _check(self.lib.bgv_verify_partial(self._h, packed.ptr(lo), hi - lo, out, codes))
         return out.raw, codes[0], codes[1]
+
+    def debug_prepare(self, sets, path: int, seed: int = 1):
+        """bgv_debug_prepare (parity hook): per set (H(m) 192 B, f 576 B, sig status,
+        pk status) from the bulk (PATH_BULK) or latency (PATH_LATENCY) kernels."""
+        packed = PackedCall([(list(sets), False)])
+        n = packed.nsets
+        h = ctypes.create_string_buffer(192 * max(1, n))
+        f = ctypes.create_string_buffer(576 * max(1, n))
+        st = (ctypes.c_int32 * max(2, 2 * n))()
+        _check(self.lib.bgv_debug_prepare(self._h, packed.sets, n, path, seed, h, f, st))
+        return [(h.raw[192 * i:192 * i + 192], f.raw[576 * i:576 * i + 576], st[2 * i], st[2 * i + 1])
+                for i in range(n)]
 
     def final_verify(self, partials: Sequence[bytes]) -> bool:
         """Product of serialized partials and one final exponentiation == 1 (bgv_final_verify)."""

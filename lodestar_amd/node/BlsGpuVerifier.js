@@ -115,18 +115,25 @@ class BlsGpuVerifier {
     };
   }
 
+  // A run leaves the queue only once the device holds it: if a put throws (e.g. a gap in the
+  // indices), that run and every later one stay queued for the next flush, and the error
+  // reaches the caller.
   flushPubkeys() {
     const p = this.pendingPubkeys;
     if (p.length === 0 || this.closed) return;
-    this.pendingPubkeys = [];
     p.sort((a, b) => a[0] - b[0]);
-    for (let i = 0; i < p.length; ) {
-      let j = i + 1;
-      while (j < p.length && p[j][0] === p[j - 1][0] + 1) j++;
-      const buf = new Uint8Array(48 * (j - i));
-      for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
-      addon.pubkeysPut(this.ctx, p[i][0], buf, 48);
-      i = j;
+    let i = 0;
+    try {
+      while (i < p.length) {
+        let j = i + 1;
+        while (j < p.length && p[j][0] === p[j - 1][0] + 1) j++;
+        const buf = new Uint8Array(48 * (j - i));
+        for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
+        addon.pubkeysPut(this.ctx, p[i][0], buf, 48);
+        i = j;
+      }
+    } finally {
+      this.pendingPubkeys = p.slice(i);
     }
   }
 

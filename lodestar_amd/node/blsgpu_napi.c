@@ -459,6 +459,14 @@ static void verify_call_js(napi_env env, napi_value js_cb, void* context, void* 
     settle(env, r);
     if (--a->inflight == 0 && !a->tsfn_released) napi_unref_threadsafe_function(env, a->tsfn);
     free_req(env, r);
+  } else {
+    /* environment teardown drained the queue: no JS to settle (the promise dies with the
+     * environment) and no env for the references (they die with it too); free the heap part */
+    free(r->refs);
+    free(r->jobs);
+    free(r->sets);
+    free(r->codes);
+    free(r);
   }
 }
 

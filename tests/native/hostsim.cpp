@@ -53,14 +53,14 @@ int hs_k_sig_body(const uint8_t* sig96, uint64_t r) {
   bool inf;
   if (g2_decompress(&a, &inf, sig96) || inf) return 0;
   if (!g2_in_subgroup(jac_from_aff(a))) return 0;
-  return !jac_is_inf(jac_mul_u64(jac_from_aff(a), r));  // r * sig for the group sum
+  return !jac_is_inf(jac_mul_glv(jac_from_aff(a), r));  // r * sig for the group sum
 }
 int hs_k_hash_body(const uint8_t* msg32) { return !jac_is_inf(hash_to_g2(msg32, 32)); }
 int hs_k_pk_body(const uint8_t* pk_aff_tl, uint32_t n_pk, uint64_t r) {
   g1_aff p = in_g1(pk_aff_tl);
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = 0; k < n_pk; ++k) acc = jac_add_aff(acc, p);
-  return !jac_is_inf(jac_mul_u64(acc, r));  // Jacobian: the Miller loop takes P projectively
+  return !jac_is_inf(jac_mul_glv(acc, r));  // Jacobian: the Miller loop takes P projectively
 }
 void hs_k_miller_body(const uint8_t* p, const uint8_t* q) {
   (void)miller_loop1(jac_from_aff(in_g1(p)), jac_from_aff(in_g2(q)));
@@ -150,6 +150,12 @@ int hs_g2_dbl(uint8_t* out, const uint8_t* a) { return g2_out(out, jac_dbl(jac_f
 int hs_g2_psi(uint8_t* out, const uint8_t* a) { return g2_out(out, g2_psi(jac_from_aff(in_g2(a)))); }
 int hs_g2_clear_cofactor(uint8_t* out, const uint8_t* a) {
   return g2_out(out, g2_clear_cofactor(jac_from_aff(in_g2(a))));
+}
+int hs_g2_mul_glv(uint8_t* out, const uint8_t* aff, uint64_t k) {
+  return g2_out(out, jac_mul_glv(jac_from_aff(in_g2(aff)), k));
+}
+int hs_g1_mul_glv(uint8_t* out, const uint8_t* aff, uint64_t k) {
+  return g1_out(out, jac_mul_glv(jac_from_aff(in_g1(aff)), k));
 }
 int hs_g1_mul_u64(uint8_t* out, const uint8_t* aff, uint64_t k) {
   return g1_out(out, jac_mul_u64(jac_from_aff(in_g1(aff)), k));
@@ -246,7 +252,7 @@ int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
   const g2_jac h_lane = g2_clear_cofactor(jac_add(q0, q1));
   *bad_out = bad;
   if (!jac_eq(h_team, h_lane)) return 0;
-  return jac_eq(tc_mul_u64_host(h_lane, k), jac_mul_u64(h_lane, k)) ? 1 : 0;
+  return jac_eq(tc_mul_glv_host(h_lane, k), jac_mul_glv(h_lane, k)) ? 1 : 0;
 }
 // the latency path's team loop (bgv_tmiller.h: table-driven twist-point rounds + team Fp12)
 void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
@@ -259,9 +265,9 @@ void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uin
 // one set through the device equation: k_prep (r pk affine, r sig Jacobian), k_miller
 // (e(r pk, H)), the group's team loop e(-G1, r sig), the product and the team final check
 int hs_verify_one(const uint8_t* pk_aff, const uint8_t* h_aff, const uint8_t* sig_aff, uint64_t r) {
-  const g1_jac pa = jac_mul_u64(jac_from_aff(in_g1(pk_aff)), r);
+  const g1_jac pa = jac_mul_glv(jac_from_aff(in_g1(pk_aff)), r);
   if (jac_is_inf(pa)) return 0;
-  const g2_jac rs = jac_mul_u64(jac_from_aff(in_g2(sig_aff)), r);
+  const g2_jac rs = jac_mul_glv(jac_from_aff(in_g2(sig_aff)), r);
   tm_emu_ops o;
   const tm_emu_t f = tm_emu_from_fp12(miller_loop1(pa, jac_from_aff(in_g2(h_aff))));
   const tm_emu_t g = tm_miller_loop<tm_emu_t>(o, jac_from_aff(g1_neg_generator()), rs);

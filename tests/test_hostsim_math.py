@@ -175,6 +175,24 @@ def test_g1_arith(L):
     assert hs.b_g1(r.raw) == o.g1_mul(p1, k)
 
 
+def test_glv_randomizer_scalar_mult(L):
+    """jac_mul_glv: r P with r = lo32(k) + hi32(k) x^2 mod the group order (the batch
+    randomizers, bls_curve.h), on G1 (endomorphism (beta x, -y)) and G2 (psi^2), equal to
+    the oracle's [r]P, including a = 0, b = 0, all-ones halves and small values."""
+    x2 = (o.X * o.X) % o.R
+    q = g2_rand_in_group()
+    p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+    r2, r1 = hs.buf(192), hs.buf(96)
+    ks = [1, 2, 1 << 32, (1 << 32) | 1, 0xFFFFFFFF, 0xFFFFFFFF00000000, 0xFFFFFFFFFFFFFFFF, 7 << 32]
+    ks += [rnd.getrandbits(64) | 1 for _ in range(3)]
+    for k in ks:
+        r = ((k & 0xFFFFFFFF) + (k >> 32) * x2) % o.R
+        assert L.hs_g2_mul_glv(r2, hs.g2_b(q), hs.ctypes.c_uint64(k))
+        assert hs.b_g2(r2.raw) == o.g2_mul(q, r), hex(k)
+        assert L.hs_g1_mul_glv(r1, hs.g1_b(p), hs.ctypes.c_uint64(k))
+        assert hs.b_g1(r1.raw) == o.g1_mul(p, r), hex(k)
+
+
 def test_hash_to_g2_pieces(L):
     msg = bytes(range(32))
     r = hs.buf(192)
@@ -285,8 +303,8 @@ def test_table_driven_team_miller_loop(L):
 
 def test_team_g2_schedules(L):
     """The latency path's team cofactor clearing and r * sig (bgv_tcurve.h, generated point
-    programs, emulated lane by lane) equal g2_clear_cofactor and jac_mul_u64 as points, for
-    random messages and 64-bit scalars (including top digits 0 and a scalar of 1)."""
+    programs, emulated lane by lane) equal g2_clear_cofactor and jac_mul_glv as points, for
+    random messages and randomizer words (including zero top digits and a word of 1)."""
     import ctypes
     for k, m in enumerate((b"a", b"tcurve", b"x" * 7)):
         msg = hashlib.sha256(m).digest()
