@@ -146,6 +146,18 @@ def cuda_sync():
         pass
 
 
+def default_batching():
+    """The library's super-batch geometry at bgv_init (bgv_api.cpp: BGV_MAX_BATCH_SLOTS,
+    BGV_COALESCE_US, BGV_IDLE_COALESCE_US), restored after each measurement that changes it."""
+    def env(name, dflt):
+        try:
+            v = int(os.environ.get(name, dflt))
+        except ValueError:
+            v = dflt
+        return v if v >= 0 else dflt
+    return env("BGV_MAX_BATCH_SLOTS", 131072), env("BGV_COALESCE_US", 2000), env("BGV_IDLE_COALESCE_US", 200)
+
+
 def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0x8192, committee=1):
     """config 4: nsets single sets over distinct validators, distinct signing roots,
     1 % corrupted at random.Random(0x8192).sample positions, three classes.  committee > 1:
@@ -190,8 +202,10 @@ def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, ste
     bcalls = super_batch_calls(steps, nsets, int(os.environ.get("BGV_DISPATCHERS", "2")))
     warm_calls = -(-warmup // bcalls) * bcalls
     ctx.set_batching(bcalls * nsets, 200000, 200000)
-    win = stream_window(step, expect, warm_calls, steps, 3 * bcalls)
-    ctx.set_batching(131072, 2000, 200)
+    try:
+        win = stream_window(step, expect, warm_calls, steps, 3 * bcalls)
+    finally:
+        ctx.set_batching(*default_batching())
     return {"config": "config4 with one signing root per %d sets (%d distinct roots + the corrupted-message "
                       "ones per %d-set batch), %d steps after %d warmup, super-batches of %d calls"
                       % (committee, -(-nsets // committee), nsets, steps, warm_calls, bcalls),
@@ -278,9 +292,11 @@ def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
     assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
     done.clear()
     ctx.set_batching(inflight * nsets, 20000, 20000)
-    with ThreadPoolExecutor(max_workers=inflight) as pool:
-        res = list(pool.map(call, range(calls)))
-    ctx.set_batching(131072, 2000, 200)
+    try:
+        with ThreadPoolExecutor(max_workers=inflight) as pool:
+            res = list(pool.map(call, range(calls)))
+    finally:
+        ctx.set_batching(*default_batching())
     assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
     done.sort()
     a, b = 2 * inflight - 1, len(done) - 1
@@ -688,7 +704,7 @@ def main():
     warm_calls = win["warm_calls"]
     cuda_sync()
     barrier()
-    ctx.set_batching(131072, 2000, 200)
+    ctx.set_batching(*default_batching())
     elapsed = barrier.max(win["elapsed"])
     lat = win["latencies"]
     stats = win["stats"]
