@@ -37,6 +37,7 @@
 
 #include "../../include/blsgpu.h"
 #include "bgv_launch.h"
+#include "bls_field.h"  // host Fp12 product of the retry rounds' complement checks
 
 // parts a failing mixed group is split into per retry round (BGV_RETRY_FANOUT env).
 // Group closings are team-parallel and cheap in latency, so bisecting (64 -> 8 -> 1)
@@ -147,6 +148,7 @@ struct Exec {
   Pinned<uint32_t> h_idx;
   Pinned<uint8_t> h_pkb;
   Pinned<int32_t> h_ss, h_ps, h_verdict;
+  Pinned<fp12_t> h_gu;  // per-group u values for the retry rounds' pattern tests
   void* d_pscratch = nullptr;  // Fp12 products of bgv_verify_partial calls
   size_t pscratch_cap = 0;
   uint8_t* d_pout = nullptr;
@@ -205,7 +207,7 @@ struct Builder {
     const uint32_t gs = group_slots();
     uint32_t aligned = (first + gs - 1) / gs * gs;
     while (L.slots.size() < aligned) pad();
-    L.groups.push_back(bgv_dgroup{aligned, 0});
+    L.groups.push_back(bgv_dgroup{aligned, 0, BGV_ALL_SLOTS});
     L.group_shared.push_back(0);
     open_group = (uint32_t)L.groups.size() - 1;
     open = true;
@@ -265,6 +267,24 @@ struct Builder {
 struct Part {  // one retry test: consecutive jobs of one failing unit, and the device groups covering them
   std::vector<size_t> jobs;
   std::vector<uint32_t> groups;  // indices into the round's merged group list
+  int pattern = -1;              // pattern test: index into Call::punits (its bit is the part's order)
+};
+
+// A failing first-pass group whose jobs all lie inside it (gossip: one-set jobs) is retried
+// by pattern tests in ONE round: test S_j = the jobs whose index in the group has bit j set,
+// j < ceil(log2 n).  The complement's verdict comes for free: the group's pairing value is
+// the product of S_j's and its complement's, so with u = gprod^((p^2+1) 3 (p^4-p^2+1)/r) (the
+// pairing value is conj(u)/u, bls_team.h tm_final_exp_u) the complement passes iff
+// u_group * conj(u_j) lies in Fp6.  A job inside any passing set is valid; every invalid
+// job lies in no passing set, so one remaining candidate is the invalid job, and two or
+// more go to the next round (usually as singletons).  k tests per failing group instead of
+// fanout-bisection's 8 + 8 over two rounds.
+struct PatternUnit {
+  uint32_t group = 0;              // the call's first-pass group
+  std::vector<size_t> jobs;        // its jobs in slot order
+  std::vector<uint64_t> jmask;     // each job's slots within the group
+  fp12_t ug;                       // the group's u from the first pass
+  std::vector<uint32_t> tests;     // round group index of S_j
 };
 
 // One bgv_verify call travelling through a dispatcher.
@@ -286,7 +306,9 @@ struct Call {
   std::vector<size_t> todo;
   std::vector<int32_t> set_sig, set_pk;
   std::vector<std::vector<size_t>> units;  // pending retry units
+  std::vector<int> unit_group;             // first-pass group of a unit from pass 1, -1 later
   std::vector<Part> parts;
+  std::vector<PatternUnit> punits;         // this round's pattern-tested units
   bgv_stats st{};
   // bgv_verify_partial: the call's Miller-loop product (576 B) and its two status codes
   uint8_t* partial_out = nullptr;
@@ -430,6 +452,7 @@ static void exec_destroy(Exec* x) {
   x->h_ss.release();
   x->h_ps.release();
   x->h_verdict.release();
+  x->h_gu.release();
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
   if (x->ev_sets) (void)hipEventDestroy(x->ev_sets);
@@ -638,6 +661,7 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
       if (unit_of_group[first_bad_shared] < 0) {
         unit_of_group[first_bad_shared] = (int)call->units.size();
         call->units.emplace_back();
+        call->unit_group.push_back(first_bad_shared);
       }
       if (!seen[j]) {
         seen[j] = 1;
@@ -651,10 +675,73 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
   for (char r : group_retried) call->st.batch_retries += r;
 }
 
-// Group testing for one retry round: split every pending unit into parts.
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg) {
+// A unit from pass 1 is pattern-testable when its jobs lie only in its group and cover every
+// slot of the group that takes part in the group's product (the others -- sets of jobs that
+// failed their precheck -- contribute 1): then a test S_j and its complement partition the
+// group's product.
+static bool pattern_eligible(const Call* call, size_t u) {
+  if (u >= call->unit_group.size() || call->unit_group[u] < 0) return false;
+  const std::vector<size_t>& jobs = call->units[u];
+  if (jobs.size() < 2) return false;
+  const uint32_t g = (uint32_t)call->unit_group[u];
+  const bgv_dgroup& G = call->L.groups[g];
+  uint64_t covered = 0;
+  for (size_t j : jobs) {
+    const auto& jg = call->L.job_groups[j];
+    if (jg.size() != 1 || jg[0] != g) return false;
+    const uint32_t off = call->L.job_first_slot[j] - G.first_slot, n = call->jobs[j].n_sets;
+    covered |= (n >= 64 ? ~0ull : ((1ull << n) - 1)) << off;
+  }
+  for (uint32_t k = 0; k < G.n_slots; ++k) {
+    if ((covered >> k) & 1) continue;
+    const int32_t si = call->L.slot_set[G.first_slot + k];
+    if (si < 0) continue;
+    const int32_t a = call->set_sig[si], q = call->set_pk[si];
+    if ((a == BGV_OK || a == BGV_ST_INFINITY) && q == BGV_OK) return false;  // live, outside the unit
+  }
+  return true;
+}
+
+// Group testing for one retry round: split every pending unit into parts.  gu_pass1: the
+// first pass's per-group u values of this call (null when no unit is pattern-testable).
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, const fp12_t* gu_pass1) {
   call->parts.clear();
-  for (const auto& u : call->units) {
+  call->punits.clear();
+  for (size_t ui = 0; ui < call->units.size(); ++ui) {
+    const auto& u = call->units[ui];
+    if (gu_pass1 && pattern_eligible(call, ui)) {
+      PatternUnit pu;
+      pu.group = (uint32_t)call->unit_group[ui];
+      const bgv_dgroup& g = call->L.groups[pu.group];
+      pu.ug = gu_pass1[pu.group];
+      std::vector<std::pair<uint32_t, size_t>> order;  // jobs in slot order
+      for (size_t j : u) order.emplace_back(call->L.job_first_slot[j], j);
+      std::sort(order.begin(), order.end());
+      for (const auto& o : order) {
+        const uint32_t off = o.first - g.first_slot, n = call->jobs[o.second].n_sets;
+        pu.jobs.push_back(o.second);
+        pu.jmask.push_back((n >= 64 ? ~0ull : ((1ull << n) - 1)) << off);
+      }
+      const size_t n = pu.jobs.size();
+      int k = 0;
+      while ((1ull << k) < n) ++k;
+      for (int b = 0; b < k; ++b) {
+        uint64_t m = 0;
+        Part part;
+        for (size_t i = 0; i < n; ++i)
+          if ((i >> b) & 1) {
+            m |= pu.jmask[i];
+            part.jobs.push_back(pu.jobs[i]);
+          }
+        pu.tests.push_back((uint32_t)rg.size());
+        part.groups.push_back((uint32_t)rg.size());
+        part.pattern = (int)call->punits.size();
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m});
+        call->parts.push_back(std::move(part));
+      }
+      call->punits.push_back(std::move(pu));
+      continue;
+    }
     const size_t k = std::min<size_t>(retry_fanout(), u.size());
     for (size_t p = 0; p < k; ++p) {
       Part part;
@@ -670,7 +757,7 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg) {
         }
         for (uint32_t off = 0; off < n; off += BGV_WAVE) {
           part.groups.push_back((uint32_t)rg.size());
-          rg.push_back(bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off)});
+          rg.push_back(bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off), BGV_ALL_SLOTS});
         }
         q = q2;
       }
@@ -678,20 +765,56 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg) {
     }
   }
   call->units.clear();
+  call->unit_group.clear();
 }
 
-static void call_after_round(Call* call, const int32_t* rv) {
-  call->st.device_groups += 0;
+// u_a * conj(u_b) in Fp6 <=> conj(u_a)/u_a == conj(u_b)/u_b: the two pairing values agree
+static bool same_pairing_value(const fp12_t& ua, const fp12_t& ub) {
+  const fp12_t v = fp12_mul(ua, fp12_conj(ub));
+  return fp2_is_zero(v.c1.c0) && fp2_is_zero(v.c1.c1) && fp2_is_zero(v.c1.c2);
+}
+
+// rv: the round's verdicts; gu: its u values (null when the round has no pattern tests)
+static void call_after_round(Call* call, const int32_t* rv, const fp12_t* gu) {
   for (const Part& part : call->parts) {
+    if (part.pattern >= 0) continue;
     bool ok = true;
     for (uint32_t g : part.groups) ok = ok && rv[g];
     if (ok || part.jobs.size() == 1) {
       for (size_t j : part.jobs) call->code[j] = ok ? 1 : 0;
     } else {
       call->units.push_back(part.jobs);
+      call->unit_group.push_back(-1);
+    }
+  }
+  for (const PatternUnit& pu : call->punits) {
+    const size_t n = pu.jobs.size(), k = pu.tests.size();
+    std::vector<char> pass_s(k), pass_c(k);
+    for (size_t b = 0; b < k; ++b) {
+      pass_s[b] = rv[pu.tests[b]] != 0;
+      pass_c[b] = gu && same_pairing_value(pu.ug, gu[pu.tests[b]]);  // the complement's value is 1
+    }
+    std::vector<size_t> cand;
+    for (size_t i = 0; i < n; ++i) {
+      bool in_passing = false;
+      for (size_t b = 0; b < k && !in_passing; ++b) in_passing = ((i >> b) & 1) ? pass_s[b] : pass_c[b];
+      if (in_passing)
+        call->code[pu.jobs[i]] = 1;
+      else
+        cand.push_back(pu.jobs[i]);
+    }
+    if (cand.size() == 1) {
+      call->code[cand[0]] = 0;  // the group failed and every invalid job is a candidate
+    } else if (cand.empty()) {
+      call->units.push_back(pu.jobs);  // inconsistent (never expected): test every job again
+      call->unit_group.push_back(-1);
+    } else {
+      call->units.push_back(cand);
+      call->unit_group.push_back(-1);
     }
   }
   call->parts.clear();
+  call->punits.clear();
 }
 
 // Run one merged super-batch of calls on one dispatcher's stream.
@@ -745,7 +868,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
         max_npk = std::max(max_npk, s.n_pk);
         slots[ns++] = s;
       }
-      for (bgv_dgroup g : call->L.groups) groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots};
+      for (bgv_dgroup g : call->L.groups) groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots, g.mask};
       if (!call->L.idx.empty()) memcpy(x.h_idx.p + ni, call->L.idx.data(), 4 * call->L.idx.size());
       ni += call->L.idx.size();
       if (!call->L.pkb.empty()) memcpy(x.h_pkb.p + npb, call->L.pkb.data(), call->L.pkb.size());
@@ -807,13 +930,22 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   if (prof) prof_add(c, x, true, true);
   t_pass1 = ms_since(tg);
   const auto tp = std::chrono::steady_clock::now();
+  std::vector<uint32_t> call_gb;  // each call's first group in the merged batch
+  bool want_gu = false;
   {
     uint32_t gb = 0;
     for (Call* call : calls) {
       call->st.device_ms += ms;
       call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb);
+      call_gb.push_back(gb);
       gb += (uint32_t)call->L.groups.size();
+      for (size_t u = 0; u < call->units.size() && !want_gu; ++u) want_gu = pattern_eligible(call, u);
     }
+  }
+  if (want_gu) {  // the first pass's u values of the groups, before a retry round reuses the array
+    HIPCHK(x.h_gu.reserve(ngroups));
+    HIPCHK(hipMemcpyAsync(x.h_gu.p, b.gu, sizeof(fp12_t) * ngroups, hipMemcpyDeviceToHost, x.close));
+    HIPCHK(hipStreamSynchronize(x.close));
   }
   {
     // bgv_verify_partial calls: the product of the call's groups (before any retry round
@@ -848,9 +980,9 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   for (;;) {
     std::vector<bgv_dgroup> rg;
     std::vector<uint32_t> base;
-    for (Call* call : calls) {
+    for (size_t k = 0; k < calls.size(); ++k) {
       base.push_back((uint32_t)rg.size());
-      call_build_parts(call, rg);
+      call_build_parts(calls[k], rg, want_gu && rounds == 0 ? x.h_gu.p + call_gb[k] : nullptr);
     }
     if (rg.empty()) break;
     ++rounds;
@@ -866,6 +998,12 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     HIPCHK(bgv_launch_groups(b, SC, true));
     HIPCHK(hipEventRecord(x.ev1, x.close));
     HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
+    bool pattern = false;
+    for (Call* call : calls) pattern = pattern || !call->punits.empty();
+    if (pattern) {
+      HIPCHK(x.h_gu.reserve(nrg));
+      HIPCHK(hipMemcpyAsync(x.h_gu.p, b.gu, sizeof(fp12_t) * nrg, hipMemcpyDeviceToHost, x.close));
+    }
     HIPCHK(hipStreamSynchronize(x.close));
     HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
     if (prof) prof_add(c, x, false, true);
@@ -876,7 +1014,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
       call->st.device_groups += mine;
       // part group indices are global to this round
-      call_after_round(call, rv);
+      call_after_round(call, rv, pattern ? x.h_gu.p : nullptr);
     }
   }
   t_retry = ms_since(tr);
@@ -1183,7 +1321,7 @@ int bgv_final_verify(bgv_ctx* c, const uint8_t* partials, size_t n, int32_t* out
     HIPCHK(hipMalloc(reinterpret_cast<void**>(&fs.dv), 4));
     fs.cap = cap;
   }
-  const bgv_dgroup g{0, (uint32_t)m};
+  const bgv_dgroup g{0, (uint32_t)m, BGV_ALL_SLOTS};
   HIPCHK(hipMemcpyAsync(fs.din, in.data(), 576 * m, hipMemcpyHostToDevice, d.stream));
   HIPCHK(hipMemcpyAsync(fs.dg, &g, sizeof(g), hipMemcpyHostToDevice, d.stream));
   HIPCHK(bgv_launch_final_verify(fs.din, (uint32_t)m, fs.vals, fs.one, fs.dg, fs.dst, fs.dv, d.stream));
@@ -1241,7 +1379,8 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
     slots.push_back(s);
   }
   for (size_t g = 0; g * BGV_WAVE < nsets; ++g)
-    groups.push_back(bgv_dgroup{(uint32_t)(g * BGV_WAVE), (uint32_t)std::min<size_t>(BGV_WAVE, nsets - g * BGV_WAVE)});
+    groups.push_back(bgv_dgroup{(uint32_t)(g * BGV_WAVE), (uint32_t)std::min<size_t>(BGV_WAVE, nsets - g * BGV_WAVE),
+                                BGV_ALL_SLOTS});
   const uint32_t nslots = (uint32_t)slots.size(), ngroups = (uint32_t)groups.size();
   std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];

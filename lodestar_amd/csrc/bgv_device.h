@@ -56,6 +56,12 @@ __device__ __forceinline__ P point_xor(const P& p) {
 
 
 
+// slot first_slot + k is in group g (the mask covers the first 64; a longer run -- the
+// partials of bgv_final_verify -- has every element in)
+__device__ __forceinline__ bool grp_has(const bgv_dgroup& g, uint32_t k) {
+  return k < g.n_slots && (k >= 64 || ((g.mask >> k) & 1));
+}
+
 // A slot takes part in its group's equation iff it is a set whose signature decoded
 // (valid or infinity) and whose pubkeys aggregated to a finite point; its signature
 // joins the group's sum only when it is not the infinity signature (blst skips those).

@@ -16,7 +16,8 @@ extern "C" {
 // barrier.
 __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                   const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
-                                  int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod) {
+                                  int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
+                                  fp12_t* __restrict__ gu) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL_TEAMS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
@@ -36,15 +37,18 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
   constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
   // the group's signature pair first, then its slots
   fp_t x = reinterpret_cast<const fp_t*>(gpair + gg)[fi];
-  fp_t y = g.n_slots ? fs[fi] : one_c;
+  fp_t y = grp_has(g, 0) ? fs[fi] : one_c;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-    const fp_t yn = k + 1 < g.n_slots ? fs[kFp12 * (k + 1) + fi] : one_c;  // next operand in flight
+    // next operand in flight (1 for a slot outside the group's mask)
+    const fp_t yn = grp_has(g, k + 1) ? fs[kFp12 * (k + 1) + fi] : one_c;
     x = o.mul(x, y);
     y = yn;
   }
   // the group's Miller-loop product, kept for cross-process partials (bgv_verify_partial)
   if (gprod && gi < ngroups && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
-  const bool one = tm_final_exp_is_one(o, x);
+  const fp_t u = tm_final_exp_u(o, x);
+  if (gu && gi < ngroups && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
+  const bool one = o.is_fp6(u);
   if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
@@ -54,7 +58,8 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
 #define BGV_FINAL12_TEAMS 5
 __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                     const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
-                                    int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod) {
+                                    int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
+                                    fp12_t* __restrict__ gu) {
   __shared__ fp_t lds[BGV_FINAL12_TEAMS + 1][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL12_TEAMS + 1];
   const int team = threadIdx.x / BGV_TEAM_COMPS, c = threadIdx.x % BGV_TEAM_COMPS;
@@ -70,17 +75,18 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   const fp_t one_c = c == 0 ? fp_one() : fp_zero();
   tm_dev_ops_t<BGV_TEAM_COMPS> o{lds[team], lds[team] + BGV_TEAM_COMPS, c, c};
   const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
-  const uint32_t ns = live ? g.n_slots : 0;
   constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
   fp_t x = reinterpret_cast<const fp_t*>(gpair + (live ? gi : ngroups - 1))[fi];
-  fp_t y = ns ? fs[fi] : one_c;
+  fp_t y = live && grp_has(g, 0) ? fs[fi] : one_c;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-    const fp_t yn = k + 1 < ns ? fs[kFp12 * (k + 1) + fi] : one_c;
+    const fp_t yn = live && grp_has(g, k + 1) ? fs[kFp12 * (k + 1) + fi] : one_c;
     x = o.mul(x, y);
     y = yn;
   }
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
-  const bool one = tm_final_exp_is_one(o, x);
+  const fp_t u = tm_final_exp_u(o, x);
+  if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
+  const bool one = o.is_fp6(u);
   if (live && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
@@ -91,7 +97,8 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
 // serial product chain; the check is unchanged.
 __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                        const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
-                                       int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod) {
+                                       int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
+                                       fp12_t* __restrict__ gu) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FINAL_TEAMS][BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
@@ -107,7 +114,7 @@ __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, ui
   const uint32_t nmax = (g.n_slots + BGV_FINAL_TEAMS - 1) / BGV_FINAL_TEAMS;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
     const uint32_t idx = team + BGV_FINAL_TEAMS * k;
-    const fp_t y = idx < g.n_slots ? fs[kFp12 * idx + fi] : one_c;
+    const fp_t y = grp_has(g, idx) ? fs[kFp12 * idx + fi] : one_c;
     x = o.mul(x, y);
   }
   if (c < BGV_TEAM_COMPS) part[team][cc] = x;
@@ -115,7 +122,9 @@ __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, ui
   x = part[0][cc];
   BGV_UNROLL for (int t = 1; t < BGV_FINAL_TEAMS; ++t) x = o.mul(x, part[t][cc]);
   if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
-  const bool one = tm_final_exp_is_one(o, x);
+  const fp_t u = tm_final_exp_u(o, x);
+  if (gu && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
+  const bool one = o.is_fp6(u);
   if (gi < ngroups && team == 0 && c == 0) verdict[gi] = one ? 1 : 0;
 }
 
@@ -187,10 +196,10 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   }
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
-                       b.verdict, b.gprod);
+                       b.verdict, b.gprod, b.gu);
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
-                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod);
+                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu);
   BGV_MARK(5);
   return hipGetLastError();
 }
@@ -214,6 +223,7 @@ hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, vo
   hipLaunchKernelGGL(k_fp12_from_bytes, dim3(nblk(n, 64)), dim3(64), 0, st, in, n, reinterpret_cast<fp12_t*>(vals),
                      status, reinterpret_cast<fp12_t*>(one));
   hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, group, 1u, reinterpret_cast<const fp12_t*>(vals),
-                     reinterpret_cast<const fp12_t*>(one), verdict, static_cast<fp12_t*>(nullptr));
+                     reinterpret_cast<const fp12_t*>(one), verdict, static_cast<fp12_t*>(nullptr),
+                     static_cast<fp12_t*>(nullptr));
   return hipGetLastError();
 }

@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
   g2_jac acc = jac_infinity<fp2_t>();
   for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+    if (!grp_has(g, k)) continue;
     const uint32_t s = g.first_slot + k;
     const int32_t ss = sig_status[s];
     if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);

@@ -97,10 +97,9 @@ __device__ __noinline__ void task_map(uint32_t s, int which, const bgv_dslot* __
   if (d.flags & BGV_SLOT_PAD) return;
   uint8_t msg[32];
   for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
-  fp2_t u0, u1, x, y;
+  fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, 32);
-  sswu_g2(&x, &y, which ? u1 : u0, fp_sqrt_minus5());
-  *out = iso_map_g2(x, y);
+  *out = iso_map_g2_jac(sswu_g2_jac(which ? u1 : u0, fp_sqrt_minus5()));
 }
 
 // task_sig's decoding half: status, and the affine point when it decodes to a finite point

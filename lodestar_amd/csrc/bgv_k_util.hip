@@ -200,7 +200,7 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 size_t bgv_slot_bytes() {
   return 2 * sizeof(g2_jac) + sizeof(g1_jac) + sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t);
 }
-size_t bgv_group_bytes() { return sizeof(g2_jac) + 2 * sizeof(fp12_t) + sizeof(int32_t); }
+size_t bgv_group_bytes() { return sizeof(g2_jac) + 3 * sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
 
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
@@ -224,6 +224,8 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   b->gpair = reinterpret_cast<fp12_t*>(q);
   q += sizeof(fp12_t) * (size_t)cap_groups;
   b->gprod = reinterpret_cast<fp12_t*>(q);
+  q += sizeof(fp12_t) * (size_t)cap_groups;
+  b->gu = reinterpret_cast<fp12_t*>(q);
   q += sizeof(fp12_t) * (size_t)cap_groups;
   b->verdict = reinterpret_cast<int32_t*>(q);
 }

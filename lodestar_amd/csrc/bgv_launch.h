@@ -49,6 +49,7 @@ struct bgv_dev_batch {
   jac_t<fp2_t>* gsum;  // per group: sum of its r_i sig_i
   fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
   fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
+  fp12_t* gu;          // per group: u = gprod^((p^2+1) 3 (p^4-p^2+1)/r); pairing value conj(u)/u
   int32_t* verdict;    // per group
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }

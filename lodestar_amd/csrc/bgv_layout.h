@@ -36,7 +36,11 @@ enum {
   BGV_ST_INFINITY = 100,  // infinity signature / pubkey: valid encoding, skipped in the product
 };
 
+// A device group: the slots first_slot + k, k < n_slots, whose bit k of mask is set (retry
+// rounds test job subsets that are not contiguous: bgv_api.cpp pattern tests).
 struct bgv_dgroup {
   uint32_t first_slot;  // multiple of BGV_WAVE
   uint32_t n_slots;     // 1..64
+  uint64_t mask;
 };
+#define BGV_ALL_SLOTS (~0ull)

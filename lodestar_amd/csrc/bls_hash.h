@@ -267,24 +267,86 @@ BGV_NOINLINE g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
   return r;
 }
 
-// Full hash_to_G2 of one message: returns Jacobian point in G2.  The two maps' 1/den
-// come from one inversion of den0 den1 (a zero den only ever meets the exceptional case,
-// which ignores its inverse; the other map's inverse then comes from its own inversion).
+// Simplified SWU on E2' straight to Jacobian coordinates, with no inversion (RFC 9380 6.6.2;
+// x = X/Z^2, y = Y/Z^3).  x1 = x1n / x1d, so gx1 = U / V with V = x1d^3, and the square root
+// of the ratio runs through the norm method of fp2_sqrt_or_z on U/V = w/n, w = U conj(V),
+// n = N(V) in Fp: w/n is a square iff w is (n^2 is), sqrt(N(w/n)) = sqrt(N(w))/n, d = d'/n,
+// and with T = n (d' n^3)^((p-3)/4)
+//     d^((p+1)/4) = d' T,   h1 d^((p-3)/4) = h1' T,   d^((p-1)/2) = d' n T^2
+// (n^(p-1) = 1), so the same two (p-3)/4 exponentiations as sqrt(g) give sqrt(U/V) and
+// the inversion of the affine map is gone.  The same point as sswu_g2 (tests/test_hostsim_math.py).
+BGV_NOINLINE g2_jac sswu_g2_jac(const fp2_t& u, const fp_t& sqrt_m5) {
+  const fp2_t Z = BGV_SSWU_Z, A = BGV_SSWU_A, B = BGV_SSWU_B;
+  const fp2_t tv1 = fp2_mul(Z, fp2_sqr(u));
+  const fp2_t tv2 = fp2_add(fp2_sqr(tv1), tv1);
+  const bool exc = fp2_is_zero(tv2);  // x1 = B / (Z A)
+  const fp2_t x1n = fp2_select(exc, fp2_neg(fp2_mul(B, fp2_add(tv2, fp2_one()))), B);
+  const fp2_t x1d = fp2_select(exc, fp2_mul(A, tv2), fp2_mul(Z, A));
+  const fp2_t d2 = fp2_sqr(x1d);
+  const fp2_t V = fp2_mul(d2, x1d);
+  const fp2_t U = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1n), fp2_mul(A, d2)), x1n), fp2_mul(B, V));
+  const fp2_t w = fp2_mul(U, fp2_conj(V));
+  const fp_t n = fp_add(fp_sqr(V.c0), fp_sqr(V.c1));
+  const fp_t nw = fp_add(fp_sqr(w.c0), fp_sqr(w.c1));
+  const fp_t e = fp_pow_p_minus_3_div_4(nw);
+  const fp_t ne = fp_mul(nw, e);
+  const bool sq = fp_eq(fp_mul(ne, e), fp_one()) || fp_is_zero(nw);
+  const fp2_t h = fp2_select(sq, fp2_mul(Z, w), w);
+  const fp_t gam = fp_select(sq, fp_mul(sqrt_m5, fp_neg(ne)), ne);
+  const fp_t d = fp_select(fp_is_zero(h.c1), fp_half(fp_add(h.c0, gam)), h.c0);
+  const fp_t T = fp_mul(n, fp_pow_p_minus_3_div_4(fp_mul(d, fp_mul(fp_sqr(n), n))));
+  const fp_t y0 = fp_mul(d, T), y1 = fp_half(fp_mul(h.c1, T));
+  const bool qr = fp_eq(fp_mul(fp_mul(d, n), fp_sqr(T)), fp_one());
+  fp2_t r;  // sqrt(gx1), or sqrt(Z gx1) when gx1 is not a square
+  r.c0 = fp_select(qr, y1, y0);
+  r.c1 = fp_select(qr, fp_neg(y0), y1);
+  // x = x1 or x2 = tv1 x1; y = r or tv1 u r (= Z u^3 sqrt(Z gx1))
+  const fp2_t xn = fp2_mul(x1n, x1d);
+  fp2_t y = fp2_select(sq, fp2_mul(fp2_mul(tv1, u), r), r);
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  g2_jac o;
+  o.x = fp2_select(sq, fp2_mul(tv1, xn), xn);
+  o.y = fp2_mul(y, V);
+  o.z = x1d;
+  return o;
+}
+
+// 3-isogeny E2' -> E2 (RFC 9380 E.3) of a Jacobian point: the rational maps in x = X/Z^2
+// homogenized with z2 = Z^2 (XN = xnum z2^3, XD = xden z2^2, YN = ynum z2^3, YD = yden z2^3),
+// x' = XN / (XD z2), y' = Y YN / (Z^3 YD); output (A D W, C B W^2, W) with A/B = x',
+// C/D = y', W = B D.
+BGV_NOINLINE g2_jac iso_map_g2_jac(const g2_jac& p) {
+  const fp2_t xnum[4] = BGV_ISO_XNUM;
+  const fp2_t xden[2] = BGV_ISO_XDEN;
+  const fp2_t ynum[4] = BGV_ISO_YNUM;
+  const fp2_t yden[3] = BGV_ISO_YDEN;
+  const fp2_t X = p.x, z2 = fp2_sqr(p.z);
+  const fp2_t z4 = fp2_sqr(z2), z6 = fp2_mul(z4, z2);
+  const fp2_t X2 = fp2_sqr(X), X3 = fp2_mul(X2, X);
+  const fp2_t X2z2 = fp2_mul(X2, z2), Xz4 = fp2_mul(X, z4);
+  const fp2_t XN = fp2_add(fp2_add(fp2_mul(xnum[3], X3), fp2_mul(xnum[2], X2z2)),
+                           fp2_add(fp2_mul(xnum[1], Xz4), fp2_mul(xnum[0], z6)));
+  const fp2_t XD = fp2_add(fp2_add(X2, fp2_mul(xden[1], fp2_mul(X, z2))), fp2_mul(xden[0], z4));
+  const fp2_t YN = fp2_add(fp2_add(fp2_mul(ynum[3], X3), fp2_mul(ynum[2], X2z2)),
+                           fp2_add(fp2_mul(ynum[1], Xz4), fp2_mul(ynum[0], z6)));
+  const fp2_t YD = fp2_add(fp2_add(X3, fp2_mul(yden[2], X2z2)), fp2_add(fp2_mul(yden[1], Xz4), fp2_mul(yden[0], z6)));
+  const fp2_t Bq = fp2_mul(XD, z2);
+  const fp2_t Dq = fp2_mul(fp2_mul(p.z, z2), YD);
+  const fp2_t Cq = fp2_mul(p.y, YN);
+  g2_jac r;
+  r.z = fp2_mul(Bq, Dq);
+  r.x = fp2_mul(fp2_mul(XN, Dq), r.z);
+  r.y = fp2_mul(fp2_mul(Cq, Bq), fp2_sqr(r.z));
+  return r;
+}
+
+// Full hash_to_G2 of one message: a Jacobian point in G2 (both maps in Jacobian form, no
+// inversion anywhere).
 BGV_NOINLINE g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, len);
   const fp_t sm5 = fp_sqrt_minus5();
-  fp2_t zu0, zu1;
-  const fp2_t d0 = sswu_den(u0, &zu0), d1 = sswu_den(u1, &zu1);
-  const bool z0 = fp2_is_zero(d0), z1 = fp2_is_zero(d1);
-  // 1/(d0 d1) with a zero factor replaced by 1
-  const fp2_t e0 = fp2_select(z0, d0, fp2_one()), e1 = fp2_select(z1, d1, fp2_one());
-  const fp2_t inv = fp2_inv(fp2_mul(e0, e1));
-  const fp2_t i0 = fp2_mul(inv, e1), i1 = fp2_mul(inv, e0);
-  fp2_t x, y;
-  sswu_finish(&x, &y, u0, zu0, d0, i0, sm5);
-  g2_jac q0 = iso_map_g2(x, y);
-  sswu_finish(&x, &y, u1, zu1, d1, i1, sm5);
-  g2_jac q1 = iso_map_g2(x, y);
+  const g2_jac q0 = iso_map_g2_jac(sswu_g2_jac(u0, sm5));
+  const g2_jac q1 = iso_map_g2_jac(sswu_g2_jac(u1, sm5));
   return g2_clear_cofactor(jac_add(q0, q1));
 }

@@ -223,8 +223,11 @@ BGV_HD E tm_pow_x(O& o, const E& a) {
   return o.conj(r);  // x < 0
 }
 
+// u = f^((p^2 + 1) 3 (p^4 - p^2 + 1) / r): the final exponentiation without its (p^6 - 1)
+// factor, whose inversion it avoids.  f^(final exp) = u^(p^6 - 1) = conj(u) / u, so the
+// pairing value is 1 iff u lies in Fp6 (conj(u) = u).
 template <class O, class E>
-BGV_HD bool tm_final_exp_is_one(O& o, const E& f) {
+BGV_HD E tm_final_exp_u(O& o, const E& f) {
   const E t = o.mul(o.frob2(f), f);               // f^(p^2 + 1)
   E a = o.mul(tm_pow_x(o, t), o.conj(t));         // t^(x-1)
   a = o.mul(tm_pow_x(o, a), o.conj(a));           // t^((x-1)^2)
@@ -232,7 +235,12 @@ BGV_HD bool tm_final_exp_is_one(O& o, const E& f) {
   E b = tm_pow_x(o, tm_pow_x(o, a));              // a^(x^2)
   b = o.mul(o.mul(b, o.frob2(a)), o.conj(a));     // a^(x^2 + p^2 - 1)
   const E t3 = o.mul(o.sqr(t), t);                // t^3
-  return o.is_fp6(o.mul(b, t3));
+  return o.mul(b, t3);
+}
+
+template <class O, class E>
+BGV_HD bool tm_final_exp_is_one(O& o, const E& f) {
+  return o.is_fp6(tm_final_exp_u(o, f));
 }
 
 // Host emulation of a team (tests): all 12 components in one value, every op

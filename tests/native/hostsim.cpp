@@ -175,6 +175,9 @@ void hs_sswu(uint8_t* out, const uint8_t* u) {
   sswu_g2(&x, &y, in_fp2(u), fp_sqrt_minus5());
   out_g2(out, g2_aff{x, y});
 }
+int hs_sswu_iso_jac(uint8_t* out, const uint8_t* u) {
+  return g2_out(out, iso_map_g2_jac(sswu_g2_jac(in_fp2(u), fp_sqrt_minus5())));
+}
 int hs_iso_map(uint8_t* out, const uint8_t* aff) {
   g2_aff a = in_g2(aff);
   return g2_out(out, iso_map_g2(a.x, a.y));
@@ -247,6 +250,10 @@ int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
   const g2_jac q0 = iso_map_g2(x, y);
   sswu_g2(&x, &y, u1, fp_sqrt_minus5());
   const g2_jac q1 = iso_map_g2(x, y);
+  // the Jacobian maps (no inversion) give the same points
+  if (!jac_eq(q0, iso_map_g2_jac(sswu_g2_jac(u0, fp_sqrt_minus5()))) ||
+      !jac_eq(q1, iso_map_g2_jac(sswu_g2_jac(u1, fp_sqrt_minus5()))))
+    return 0;
   bool bad;
   const g2_jac h_team = tc_clear_cofactor_host(q0, q1, &bad);
   const g2_jac h_lane = g2_clear_cofactor(jac_add(q0, q1));

@@ -207,6 +207,31 @@ def test_hash_to_g2_pieces(L):
     assert hs.b_g2(r.raw) == o.iso_map_g2(pt)
 
 
+def test_sswu_iso_jacobian_without_inversion(L):
+    """sswu_g2_jac + iso_map_g2_jac (the kernels' maps: Jacobian, no inversion, the square
+    root of the ratio gx1 = U/V through the norm method) equal the oracle's affine maps, for
+    random u (both square / non-square branches), u = 0 (the exceptional x1 = B/(ZA)) and
+    the hash_to_field outputs."""
+    r = hs.buf(192)
+    msg = bytes(range(32))
+    us = list(o.hash_to_field_fp2(msg, o.DST_POP)) + [rfp2() for _ in range(12)] + [(0, 0), (1, 0), (0, 1)]
+    branches = set()
+    for u in us:
+        assert L.hs_sswu_iso_jac(r, hs.fp2_b(u))
+        assert hs.b_g2(r.raw) == o.iso_map_g2(o.sswu_g2(u)), u
+        branches.add(o.f2_is_square(o.f2_add(o.f2_mul(o.f2_add(o.f2_sqr(_x1(u)), o.SSWU_A), _x1(u)), o.SSWU_B)))
+    assert branches == {True, False}
+
+
+def _x1(u):
+    """RFC 9380 6.6.2 x1 of the simplified SWU map (the oracle's formulas)"""
+    tv1 = o.f2_mul(o.SSWU_Z, o.f2_sqr(u))
+    tv2 = o.f2_add(o.f2_sqr(tv1), tv1)
+    if o.f2_is_zero(tv2):
+        return o.f2_mul(o.SSWU_B, o.f2_inv(o.f2_mul(o.SSWU_Z, o.SSWU_A)))
+    return o.f2_mul(o.f2_mul(o.f2_neg(o.SSWU_B), o.f2_inv(o.SSWU_A)), o.f2_add((1, 0), o.f2_inv(tv2)))
+
+
 @pytest.mark.parametrize("msg", [b"", b"abc", bytes(32), bytes([7]) * 32, bytes(range(100))])
 def test_hash_to_g2(L, msg):
     aff, comp = hs.buf(192), hs.buf(96)
