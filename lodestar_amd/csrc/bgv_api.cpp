@@ -148,7 +148,8 @@ struct Exec {
   Pinned<uint32_t> h_idx;
   Pinned<uint8_t> h_pkb;
   Pinned<int32_t> h_ss, h_ps, h_verdict;
-  Pinned<fp12_t> h_gu;  // per-group u values for the retry rounds' pattern tests
+  fp12_t* d_gu1 = nullptr;  // the first pass's per-group u values, kept for the retry rounds' pattern tests
+  size_t gu1_cap = 0;
   void* d_pscratch = nullptr;  // Fp12 products of bgv_verify_partial calls
   size_t pscratch_cap = 0;
   uint8_t* d_pout = nullptr;
@@ -279,13 +280,20 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // job lies in no passing set, so one remaining candidate is the invalid job, and two or
 // more go to the next round (usually as singletons).  k tests per failing group instead of
 // fanout-bisection's 8 + 8 over two rounds.
+//
+// The remaining candidates (two or more invalid jobs: 2^h of them for two jobs whose indices
+// differ in h bits) are tested one job per device group in the next round, so a failing
+// group is resolved in at most two rounds: a round costs about the same latency whether it
+// tests hundreds or thousands of groups, while a second pattern round over the candidates
+// need not shrink them (two invalid jobs at the first and last candidate index).
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
   std::vector<size_t> jobs;        // its jobs in slot order
-  std::vector<uint64_t> jmask;     // each job's slots within the group
-  fp12_t ug;                       // the group's u from the first pass
   std::vector<uint32_t> tests;     // round group index of S_j
 };
+// units from the first pass of at most this many jobs (not pattern-testable) are tested one
+// job per device group
+static const size_t kSingletonMax = 8;
 
 // One bgv_verify call travelling through a dispatcher.
 struct Call {
@@ -306,7 +314,8 @@ struct Call {
   std::vector<size_t> todo;
   std::vector<int32_t> set_sig, set_pk;
   std::vector<std::vector<size_t>> units;  // pending retry units
-  std::vector<int> unit_group;             // first-pass group of a unit from pass 1, -1 later
+  std::vector<int> unit_group;             // first-pass group the unit's jobs lie in (-1: not known)
+  std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through
   std::vector<Part> parts;
   std::vector<PatternUnit> punits;         // this round's pattern-tested units
   bgv_stats st{};
@@ -452,7 +461,7 @@ static void exec_destroy(Exec* x) {
   x->h_ss.release();
   x->h_ps.release();
   x->h_verdict.release();
-  x->h_gu.release();
+  if (x->d_gu1) (void)hipFree(x->d_gu1);
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
   if (x->ev_sets) (void)hipEventDestroy(x->ev_sets);
@@ -652,7 +661,7 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
     bool ok = true;
     int first_bad_shared = -1;
     for (uint32_t g : L.job_groups[j])
-      if (!verdict[g]) {
+      if (!(verdict[g] & 1)) {
         ok = false;
         if (L.group_shared[g] && first_bad_shared < 0) first_bad_shared = (int)g;
       }
@@ -662,6 +671,7 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
         unit_of_group[first_bad_shared] = (int)call->units.size();
         call->units.emplace_back();
         call->unit_group.push_back(first_bad_shared);
+        call->unit_rounds.push_back(0);
       }
       if (!seen[j]) {
         seen[j] = 1;
@@ -702,25 +712,43 @@ static bool pattern_eligible(const Call* call, size_t u) {
   return true;
 }
 
-// Group testing for one retry round: split every pending unit into parts.  gu_pass1: the
-// first pass's per-group u values of this call (null when no unit is pattern-testable).
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, const fp12_t* gu_pass1) {
+// A job's slots within its (single) group g, as a device-group mask
+static uint64_t job_mask(const Call* call, size_t j, const bgv_dgroup& g) {
+  const uint32_t off = call->L.job_first_slot[j] - g.first_slot, n = call->jobs[j].n_sets;
+  return (n >= 64 ? ~0ull : ((1ull << n) - 1)) << off;
+}
+
+// every job of the unit lies in the call's group g alone
+static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int g) {
+  if (g < 0) return false;
+  for (size_t j : jobs) {
+    const auto& jg = call->L.job_groups[j];
+    if (jg.size() != 1 || jg[0] != (uint32_t)g) return false;
+  }
+  return true;
+}
+
+// Group testing for one retry round: split every pending unit into parts.  gb: the call's
+// first group in the batch when the first pass's u values are on the device (pattern tests
+// possible), else -1.
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb) {
   call->parts.clear();
   call->punits.clear();
   for (size_t ui = 0; ui < call->units.size(); ++ui) {
     const auto& u = call->units[ui];
-    if (gu_pass1 && pattern_eligible(call, ui)) {
+    const int ug = call->unit_group[ui], urounds = call->unit_rounds[ui];
+    const bool in_group = unit_in_group(call, u, ug);
+    if (gb >= 0 && in_group && urounds == 0 && u.size() >= 2 && pattern_eligible(call, ui)) {
       PatternUnit pu;
-      pu.group = (uint32_t)call->unit_group[ui];
+      pu.group = (uint32_t)ug;
       const bgv_dgroup& g = call->L.groups[pu.group];
-      pu.ug = gu_pass1[pu.group];
       std::vector<std::pair<uint32_t, size_t>> order;  // jobs in slot order
       for (size_t j : u) order.emplace_back(call->L.job_first_slot[j], j);
       std::sort(order.begin(), order.end());
+      std::vector<uint64_t> jmask;
       for (const auto& o : order) {
-        const uint32_t off = o.first - g.first_slot, n = call->jobs[o.second].n_sets;
         pu.jobs.push_back(o.second);
-        pu.jmask.push_back((n >= 64 ? ~0ull : ((1ull << n) - 1)) << off);
+        jmask.push_back(job_mask(call, o.second, g));
       }
       const size_t n = pu.jobs.size();
       int k = 0;
@@ -730,16 +758,28 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, const fp12
         Part part;
         for (size_t i = 0; i < n; ++i)
           if ((i >> b) & 1) {
-            m |= pu.jmask[i];
+            m |= jmask[i];
             part.jobs.push_back(pu.jobs[i]);
           }
         pu.tests.push_back((uint32_t)rg.size());
         part.groups.push_back((uint32_t)rg.size());
         part.pattern = (int)call->punits.size();
-        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m});
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1), 0});
         call->parts.push_back(std::move(part));
       }
       call->punits.push_back(std::move(pu));
+      continue;
+    }
+    if (in_group && (urounds > 0 || u.size() <= kSingletonMax)) {
+      // one device group per job, each masked to the job's slots: every verdict in this round
+      const bgv_dgroup& g = call->L.groups[ug];
+      for (size_t j : u) {
+        Part part;
+        part.jobs.push_back(j);
+        part.groups.push_back((uint32_t)rg.size());
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, job_mask(call, j, g), 0, 0});
+        call->parts.push_back(std::move(part));
+      }
       continue;
     }
     const size_t k = std::min<size_t>(retry_fanout(), u.size());
@@ -757,7 +797,8 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, const fp12
         }
         for (uint32_t off = 0; off < n; off += BGV_WAVE) {
           part.groups.push_back((uint32_t)rg.size());
-          rg.push_back(bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off), BGV_ALL_SLOTS});
+          rg.push_back(
+              bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off), BGV_ALL_SLOTS, 0, 0});
         }
         q = q2;
       }
@@ -766,51 +807,48 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, const fp12
   }
   call->units.clear();
   call->unit_group.clear();
+  call->unit_rounds.clear();
 }
 
-// u_a * conj(u_b) in Fp6 <=> conj(u_a)/u_a == conj(u_b)/u_b: the two pairing values agree
-static bool same_pairing_value(const fp12_t& ua, const fp12_t& ub) {
-  const fp12_t v = fp12_mul(ua, fp12_conj(ub));
-  return fp2_is_zero(v.c1.c0) && fp2_is_zero(v.c1.c1) && fp2_is_zero(v.c1.c2);
+static bool trace_on() {
+  static const bool v = getenv("BGV_TRACE") != nullptr;
+  return v;
 }
 
-// rv: the round's verdicts; gu: its u values (null when the round has no pattern tests)
-static void call_after_round(Call* call, const int32_t* rv, const fp12_t* gu) {
+// rv: the round's verdict bits (bgv_layout.h: bit 0 the group passes, bit 1 its pairing value
+// equals its reference's, i.e. the complement passes)
+static void call_after_round(Call* call, const int32_t* rv) {
   for (const Part& part : call->parts) {
     if (part.pattern >= 0) continue;
     bool ok = true;
-    for (uint32_t g : part.groups) ok = ok && rv[g];
+    for (uint32_t g : part.groups) ok = ok && (rv[g] & 1);
     if (ok || part.jobs.size() == 1) {
       for (size_t j : part.jobs) call->code[j] = ok ? 1 : 0;
     } else {
       call->units.push_back(part.jobs);
       call->unit_group.push_back(-1);
+      call->unit_rounds.push_back(0);
     }
   }
   for (const PatternUnit& pu : call->punits) {
     const size_t n = pu.jobs.size(), k = pu.tests.size();
-    std::vector<char> pass_s(k), pass_c(k);
-    for (size_t b = 0; b < k; ++b) {
-      pass_s[b] = rv[pu.tests[b]] != 0;
-      pass_c[b] = gu && same_pairing_value(pu.ug, gu[pu.tests[b]]);  // the complement's value is 1
-    }
     std::vector<size_t> cand;
     for (size_t i = 0; i < n; ++i) {
-      bool in_passing = false;
-      for (size_t b = 0; b < k && !in_passing; ++b) in_passing = ((i >> b) & 1) ? pass_s[b] : pass_c[b];
+      bool in_passing = false;  // in S_b (bit b of i set) or its complement, and that set passed
+      for (size_t b = 0; b < k && !in_passing; ++b) in_passing = (rv[pu.tests[b]] >> (((i >> b) & 1) ? 0 : 1)) & 1;
       if (in_passing)
         call->code[pu.jobs[i]] = 1;
       else
         cand.push_back(pu.jobs[i]);
     }
+    if (trace_on()) fprintf(stderr, "[bgv]   pattern unit: %zu jobs, %zu tests, %zu candidates\n", n, k, cand.size());
     if (cand.size() == 1) {
       call->code[cand[0]] = 0;  // the group failed and every invalid job is a candidate
-    } else if (cand.empty()) {
-      call->units.push_back(pu.jobs);  // inconsistent (never expected): test every job again
-      call->unit_group.push_back(-1);
     } else {
-      call->units.push_back(cand);
-      call->unit_group.push_back(-1);
+      // two or more invalid jobs (or, never expected, none left: test every job alone)
+      call->units.push_back(cand.empty() ? pu.jobs : cand);
+      call->unit_group.push_back((int)pu.group);
+      call->unit_rounds.push_back(1);
     }
   }
   call->parts.clear();
@@ -818,10 +856,6 @@ static void call_after_round(Call* call, const int32_t* rv, const fp12_t* gu) {
 }
 
 // Run one merged super-batch of calls on one dispatcher's stream.
-static bool trace_on() {
-  static const bool v = getenv("BGV_TRACE") != nullptr;
-  return v;
-}
 static double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
@@ -943,9 +977,8 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     }
   }
   if (want_gu) {  // the first pass's u values of the groups, before a retry round reuses the array
-    HIPCHK(x.h_gu.reserve(ngroups));
-    HIPCHK(hipMemcpyAsync(x.h_gu.p, b.gu, sizeof(fp12_t) * ngroups, hipMemcpyDeviceToHost, x.close));
-    HIPCHK(hipStreamSynchronize(x.close));
+    if ((rc = grow(&x.d_gu1, &x.gu1_cap, ngroups))) return rc;
+    HIPCHK(hipMemcpyAsync(x.d_gu1, b.gu, sizeof(fp12_t) * ngroups, hipMemcpyDeviceToDevice, x.close));
   }
   {
     // bgv_verify_partial calls: the product of the call's groups (before any retry round
@@ -982,7 +1015,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     std::vector<uint32_t> base;
     for (size_t k = 0; k < calls.size(); ++k) {
       base.push_back((uint32_t)rg.size());
-      call_build_parts(calls[k], rg, want_gu && rounds == 0 ? x.h_gu.p + call_gb[k] : nullptr);
+      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1);
     }
     if (rg.empty()) break;
     ++rounds;
@@ -994,19 +1027,23 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     int32_t* rv = x.h_verdict.p;
     HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
     b = make_batch(d, x, nslots, nrg);
+    bool pattern = false;
+    for (Call* call : calls) pattern = pattern || !call->punits.empty();
+    if (pattern) b.gu1 = x.d_gu1;
     HIPCHK(hipEventRecord(x.ev0, x.close));
     HIPCHK(bgv_launch_groups(b, SC, true));
     HIPCHK(hipEventRecord(x.ev1, x.close));
     HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
-    bool pattern = false;
-    for (Call* call : calls) pattern = pattern || !call->punits.empty();
-    if (pattern) {
-      HIPCHK(x.h_gu.reserve(nrg));
-      HIPCHK(hipMemcpyAsync(x.h_gu.p, b.gu, sizeof(fp12_t) * nrg, hipMemcpyDeviceToHost, x.close));
-    }
     HIPCHK(hipStreamSynchronize(x.close));
     HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
     if (prof) prof_add(c, x, false, true);
+    if (trace_on()) {
+      size_t npt = 0;
+      for (Call* call : calls)
+        for (const PatternUnit& pu : call->punits) npt += pu.tests.size();
+      fprintf(stderr, "[bgv]  round %d: %u groups (%zu pattern tests), device %.2f ms, since round start %.1f ms\n",
+              rounds, nrg, npt, ms, ms_since(tr));
+    }
     for (size_t k = 0; k < calls.size(); ++k) {
       Call* call = calls[k];
       call->st.device_ms += ms;
@@ -1014,7 +1051,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
       call->st.device_groups += mine;
       // part group indices are global to this round
-      call_after_round(call, rv, pattern ? x.h_gu.p : nullptr);
+      call_after_round(call, rv);
     }
   }
   t_retry = ms_since(tr);

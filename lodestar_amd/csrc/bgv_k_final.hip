@@ -6,6 +6,21 @@
 #include "bgv_team_dev.h"
 
 
+// A group's verdict bits from its u (bls_team.h tm_final_exp_u; pairing value conj(u)/u):
+// bit 0: the pairing value is 1 (u in Fp6).  bit 1 (gu1 given: a retry round with pattern
+// tests): it equals the value of the first-pass group ref1 - 1, i.e. u_ref conj(u) lies in
+// Fp6 -- the rest of that group, whose value is the quotient, passes.  gu1 is uniform over
+// the grid, so every lane of a block takes the same branch and reaches the same barriers.
+template <class O>
+__device__ int32_t verdict_bits(O& o, const fp_t& u, const bgv_dgroup& g, const fp12_t* __restrict__ gu1, int fi) {
+  int32_t v = o.is_fp6(u) ? 1 : 0;
+  if (gu1) {
+    const fp_t ur = g.ref1 ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : u;
+    if (o.is_fp6(o.mul(ur, o.conj(u))) && g.ref1) v |= 2;
+  }
+  return v;
+}
+
 extern "C" {
 
 // One team per device group (first pass: the groups of the layout; retry rounds: parts of
@@ -17,7 +32,7 @@ extern "C" {
 __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                   const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                   int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
-                                  fp12_t* __restrict__ gu) {
+                                  fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL_TEAMS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
@@ -48,8 +63,8 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
   if (gprod && gi < ngroups && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && gi < ngroups && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const bool one = o.is_fp6(u);
-  if (gi < ngroups && c == 0) verdict[gi] = one ? 1 : 0;
+  const int32_t v = verdict_bits(o, u, g, gu1, fi);
+  if (gi < ngroups && c == 0) verdict[gi] = v;
 }
 
 // k_final on teams of 12 lanes, five per wave (lanes 60..63 run a sixth, idle team on LDS
@@ -59,7 +74,7 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
 __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                     const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                     int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
-                                    fp12_t* __restrict__ gu) {
+                                    fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1) {
   __shared__ fp_t lds[BGV_FINAL12_TEAMS + 1][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL12_TEAMS + 1];
   const int team = threadIdx.x / BGV_TEAM_COMPS, c = threadIdx.x % BGV_TEAM_COMPS;
@@ -86,8 +101,8 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const bool one = o.is_fp6(u);
-  if (live && c == 0) verdict[gi] = one ? 1 : 0;
+  const int32_t v = verdict_bits(o, u, g, gu1, fi);
+  if (live && c == 0) verdict[gi] = v;
 }
 
 // The latency path's closing (small calls): one block of 4 teams per group.  Team t
@@ -98,7 +113,7 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
 __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                        const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                        int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
-                                       fp12_t* __restrict__ gu) {
+                                       fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FINAL_TEAMS][BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
@@ -124,8 +139,8 @@ __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, ui
   if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const bool one = o.is_fp6(u);
-  if (gi < ngroups && team == 0 && c == 0) verdict[gi] = one ? 1 : 0;
+  const int32_t v = verdict_bits(o, u, g, gu1, fi);
+  if (gi < ngroups && team == 0 && c == 0) verdict[gi] = v;
 }
 
 // Products of runs of Fp12 values (cross-process partials): team t of the
@@ -196,10 +211,10 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   }
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
-                       b.verdict, b.gprod, b.gu);
+                       b.verdict, b.gprod, b.gu, b.gu1);
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
-                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu);
+                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1);
   BGV_MARK(5);
   return hipGetLastError();
 }
@@ -224,6 +239,6 @@ hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, vo
                      status, reinterpret_cast<fp12_t*>(one));
   hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, group, 1u, reinterpret_cast<const fp12_t*>(vals),
                      reinterpret_cast<const fp12_t*>(one), verdict, static_cast<fp12_t*>(nullptr),
-                     static_cast<fp12_t*>(nullptr));
+                     static_cast<fp12_t*>(nullptr), static_cast<const fp12_t*>(nullptr));
   return hipGetLastError();
 }

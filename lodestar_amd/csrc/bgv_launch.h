@@ -50,7 +50,10 @@ struct bgv_dev_batch {
   fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
   fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
   fp12_t* gu;          // per group: u = gprod^((p^2+1) 3 (p^4-p^2+1)/r); pairing value conj(u)/u
-  int32_t* verdict;    // per group
+  // retry rounds with pattern tests: the first pass's u values (a copy of its gu), indexed by
+  // bgv_dgroup.ref1 - 1; null otherwise
+  const fp12_t* gu1;
+  int32_t* verdict;    // per group: bit 0 = the group passes, bit 1 = its pairing value equals ref's
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
 #endif

@@ -37,10 +37,15 @@ enum {
 };
 
 // A device group: the slots first_slot + k, k < n_slots, whose bit k of mask is set (retry
-// rounds test job subsets that are not contiguous: bgv_api.cpp pattern tests).
+// rounds test job subsets that are not contiguous: bgv_api.cpp pattern tests).  ref1 != 0
+// names the first-pass group (index ref1 - 1 of the batch) whose pairing value this group's
+// is compared with: the closing then also reports whether the two values agree, i.e. whether
+// the rest of that group (its complement) passes (verdict bit 1).
 struct bgv_dgroup {
   uint32_t first_slot;  // multiple of BGV_WAVE
   uint32_t n_slots;     // 1..64
   uint64_t mask;
+  uint32_t ref1;
+  uint32_t reserved;
 };
 #define BGV_ALL_SLOTS (~0ull)

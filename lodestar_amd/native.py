@@ -114,6 +114,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_deposits_verify": ([P, P, P, P, SZ, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
+            if name == "bgv_debug_prepare" and path != os.path.join(HERE, "libblsgpu.so") and \
+                    not hasattr(lib, name):
+                continue  # parity hook absent from an older A/B build (tools/gpu/ab.sh)
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
