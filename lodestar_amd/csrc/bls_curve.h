@@ -287,7 +287,7 @@ BGV_NOINLINE jac_t<F> jac_mul_x_abs(const jac_t<F>& p) {
     acc = jac_dbl(acc);
     if ((X >> i) & 1) acc = jac_add(acc, pm[bgv_opaque0()]);
   }
-  return acc;
+  return jac_t<F>{acc.x, acc.y, acc.z};  // not NRVO: acc would live in the caller's return slot (scratch)
 }
 
 // ---------------------------------------------------------------------------
@@ -372,7 +372,7 @@ BGV_NOINLINE jac_t<F> jac_mul_glv(const jac_t<F>& p, uint64_t k) {
     const jac_t<F> sb = jac_add(acc, jac_endo_x2(tab[db]));
     acc = jac_select(db != 0u, acc, sb);
   }
-  return acc;
+  return jac_t<F>{acc.x, acc.y, acc.z};  // not NRVO (see jac_mul_x_abs)
 }
 
 BGV_HD bool g2_aff_on_curve(const g2_aff& a) {
