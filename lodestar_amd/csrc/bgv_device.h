@@ -73,6 +73,14 @@ __device__ __forceinline__ bool slot_live(const bgv_dslot& d, int32_t ss, int32_
 
 static inline unsigned nblk(uint32_t n, unsigned t) { return (n + t - 1) / t; }
 
+// sets up to which the latency path's team work runs one set per block and task (k_prep_wide,
+// 4 blocks per set) instead of four sets per block (k_prep_team), and the first pass pairs
+// each signature on its own (bgv_sig_pairs): a couple of rounds of waves on the chip
+#define BGV_PREP_WIDE_MAX 340
+// pairs up to which the latency path runs one Miller loop per block (k_miller_wide) instead of
+// four (k_miller_team)
+#define BGV_MILLER_WIDE_MAX 1024
+
 // Latency path (small calls): at most this many pairs (sets + groups) take the split
 // k_prep_a / k_prep_team and the team Miller loop instead of one lane per set and task, which
 // wins while the chip would otherwise sit mostly idle (one lane per set runs ~13 ms in

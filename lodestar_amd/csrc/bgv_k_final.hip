@@ -107,15 +107,18 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
 
 // The latency path's closing (small calls): one block of 4 teams per group.  Team t
 // multiplies the group's slots t, t + 4, ... (team 0 also the signature pair), the four
-// partial products meet in LDS and every team forms the same product in the same order
-// and runs the final-exponentiation check on it (team 0 reports).  A quarter of k_final's
-// serial product chain; the check is unchanged.
+// partial products meet in LDS and every team forms the same product in the same order (a
+// quarter of k_final's serial product chain).  The final exponentiation then runs on the
+// whole block with each coefficient's products split over four lanes (tm_wide_ops): 2 + 1
+// double-width products per lane and squaring instead of 7 + 1.
 __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                        const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                        int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
-                                       fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1) {
+                                       fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
+                                       const fp12_t* __restrict__ fsig) {
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FINAL_TEAMS][BGV_TEAM_COMPS];
+  __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[4 * BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
   const uint32_t gi = blockIdx.x;
@@ -125,22 +128,33 @@ __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, ui
   tm_dev_ops o{lds[team], lds[team] + BGV_TEAM_COMPS, c, cc};
   const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
   constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
-  fp_t x = team == 0 ? reinterpret_cast<const fp_t*>(gpair + (gi < ngroups ? gi : ngroups - 1))[fi] : one_c;
+  // the group's signature pair, or (fsig: bgv_sig_pairs) each slot's own
+  fp_t x = team == 0 && !fsig ? reinterpret_cast<const fp_t*>(gpair + (gi < ngroups ? gi : ngroups - 1))[fi] : one_c;
+  const fp_t* ss = fsig ? reinterpret_cast<const fp_t*>(fsig + g.first_slot) : nullptr;
   const uint32_t nmax = (g.n_slots + BGV_FINAL_TEAMS - 1) / BGV_FINAL_TEAMS;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
     const uint32_t idx = team + BGV_FINAL_TEAMS * k;
-    const fp_t y = grp_has(g, idx) ? fs[kFp12 * idx + fi] : one_c;
+    const bool in = grp_has(g, idx);
+    const fp_t y = in ? fs[kFp12 * idx + fi] : one_c;
     x = o.mul(x, y);
+    if (ss) x = o.mul(x, in ? ss[kFp12 * idx + fi] : one_c);  // grid-uniform branch
   }
   if (c < BGV_TEAM_COMPS) part[team][cc] = x;
   __syncthreads();
   x = part[0][cc];
   BGV_UNROLL for (int t = 1; t < BGV_FINAL_TEAMS; ++t) x = o.mul(x, part[t][cc]);
   if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
-  const fp_t u = tm_final_exp_u(o, x);
-  if (gu && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const int32_t v = verdict_bits(o, u, g, gu1, fi);
-  if (gi < ngroups && team == 0 && c == 0) verdict[gi] = v;
+  // the final exponentiation on the whole block with the wide products (bgv_team_dev.h)
+  if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
+  __syncthreads();
+  const int wc = threadIdx.x % BGV_TEAM_COMPS, wq = threadIdx.x / BGV_TEAM_COMPS;
+  tm_wide_ops ow{WA, WB, WP, wc, wq};
+  const fp_t xw = W[wc];
+  const int wfi = tm_fp_index(wc);
+  const fp_t u = tm_final_exp_u(ow, xw);
+  if (gu && gi < ngroups && wq == 0) reinterpret_cast<fp_t*>(gu + gi)[wfi] = u;
+  const int32_t v = verdict_bits(ow, u, g, gu1, wfi);
+  if (gi < ngroups && threadIdx.x == 0) verdict[gi] = v;
 }
 
 // Products of runs of Fp12 values (cross-process partials): team t of the
@@ -211,7 +225,8 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   }
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
-                       b.verdict, b.gprod, b.gu, b.gu1);
+                       b.verdict, b.gprod, b.gu, b.gu1,
+                       !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1);

@@ -12,6 +12,7 @@
 #include "bgv_device.h"
 #include "bgv_team_dev.h"
 #include "bgv_tmiller.h"
+#include "bgv_tround_dev.h"
 
 static __constant__ uint8_t kTmProg[TMP_TABLE_BYTES] = TMP_TABLE_INIT;
 
@@ -162,7 +163,101 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
   }
 }
 
+// The same pairs with one pair per 64-lane block for the smallest calls: the twist-point
+// rounds of k_miller_team as four-part instructions on all 64 lanes (bgv_tround_dev.h), and
+// the Fp12 accumulator with the wide products (bgv_team_dev.h tm_wide_ops: each coefficient's
+// double-width products split over four lanes), so a doubling step waits 6 + 3 + 3 product
+// latencies instead of 10 + 8 + 7.  Same formulas, same field element as k_miller_team.
+// rsig non-null (bgv_sig_pairs): blocks [nslots, 2 nslots) pair the slots' own r_i sig_i with
+// -G1 into fsig instead of pairing group sums.
+__global__ void __launch_bounds__(64) k_miller_wide(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                    const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                                    const int32_t* __restrict__ sig_status,
+                                                    const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
+                                                    uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                                    fp12_t* __restrict__ gpair, const g2_jac* __restrict__ rsig,
+                                                    fp12_t* __restrict__ fsig) {
+  __shared__ uint8_t prog[TMP_TABLE_BYTES];
+  __shared__ fp_t Sm[TMP_NSLOT];
+  __shared__ fp_t WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[4 * BGV_TEAM_COMPS], RP[64];
+  for (int i = threadIdx.x; i < TMP_TABLE_BYTES; i += 64) prog[i] = kTmProg[i];
+  const int lane = threadIdx.x, c = lane % BGV_TEAM;  // c: lane of the twist-point rounds (< 16)
+  const uint32_t uu = blockIdx.x;                     // grid = exactly nslots + ngroups blocks
+  const bool set_pair = uu < nslots;
+  bool live;
+  const fp_t* qsrc;
+  const uint32_t j = uu - nslots;
+  if (set_pair) {
+    live = slot_live(slots[uu], sig_status[uu], pk_status[uu]);
+    qsrc = reinterpret_cast<const fp_t*>(h + slots[uu].hsrc);
+  } else if (rsig) {  // the slot's own signature pair (an infinity signature is skipped: 1)
+    live = slot_live(slots[j], sig_status[j], pk_status[j]) && sig_status[j] == BGV_ST_OK;
+    qsrc = reinterpret_cast<const fp_t*>(rsig + j);
+  } else {
+    qsrc = reinterpret_cast<const fp_t*>(gsum + j);
+    live = !jac_is_inf(gsum[j]);
+  }
+  if (lane < 6) {
+    const fp_t v = live ? qsrc[lane] : fp_zero();
+    Sm[TMP_S_QX + lane] = v;
+    Sm[TMP_S_BANK0 + lane] = v;
+  } else if (lane < 9) {
+    const g1_jac P = set_pair ? rpk[uu] : jac_from_aff(g1_neg_generator());
+    const fp_t v = lane == 6 ? fp_neg(fp_mul(P.x, P.z)) : (lane == 7 ? P.y : fp_mul(fp_sqr(P.z), P.z));
+    Sm[lane == 6 ? TMP_S_XN : (lane == 7 ? TMP_S_YP : TMP_S_ZP3)] = live ? v : fp_zero();
+  } else if (lane == 9) {
+    Sm[TMP_S_ONE] = fp_one();
+  }
+  __syncthreads();
+  tr_wide_engine eng{prog, Sm, RP, c, lane / BGV_TEAM, false};
+  auto run = [&](int off) { eng.run(off); };
+  tm_wide_ops o{WA, WB, WP, lane % BGV_TEAM_COMPS, lane / BGV_TEAM_COMPS};
+  run(TMP_INIT);
+  run(TMP_DBL0);
+  int bank = 1;
+  fp2_t l0 = {Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]}, l1 = {Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]},
+        l3 = {Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+  fp_t x = o.line(l0, l1, l3);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (tmp_add_at(i)) {
+      run(bank ? TMP_ADD1 : TMP_ADD0);
+      bank ^= 1;
+      l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
+      l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
+      l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+      x = o.mul_line(x, l0, l1, l3);
+    }
+    x = o.sqr(x);
+    run(bank ? TMP_DBL1 : TMP_DBL0);
+    bank ^= 1;
+    l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
+    l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
+    l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+    x = o.mul_line(x, l0, l1, l3);
+  }
+  x = o.conj(x);
+  if (lane < BGV_TEAM_COMPS) {
+    fp12_t* dst = set_pair ? f + uu : (rsig ? fsig + j : gpair + j);
+    reinterpret_cast<fp_t*>(dst)[tm_fp_index(lane)] = live ? x : (lane == 0 ? fp_one() : fp_zero());
+  }
+}
+
 }  // extern "C"
+
+bool bgv_sig_pairs(const bgv_dev_batch& b) {
+  return bgv_use_latency(b, b.nslots + b.ngroups) && b.nslots <= BGV_PREP_WIDE_MAX;
+}
+
+static void launch_miller_latency(const bgv_dev_batch& b, uint32_t nslots, uint32_t ngroups, hipStream_t st) {
+  const uint32_t total = nslots + ngroups;
+  if (total <= BGV_MILLER_WIDE_MAX)
+    hipLaunchKernelGGL(k_miller_wide, dim3(total), dim3(64), 0, st, b.slots, nslots, b.rpk, b.h, b.sig_status,
+                       b.pk_status, b.f, ngroups, b.gsum, b.gpair, static_cast<const g2_jac*>(nullptr),
+                       static_cast<fp12_t*>(nullptr));
+  else
+    hipLaunchKernelGGL(k_miller_team, dim3(nblk(total, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, nslots, b.rpk,
+                       b.h, b.sig_status, b.pk_status, b.f, ngroups, b.gsum, b.gpair);
+}
 
 // lanes of one k_miller round: one wave of 64 on each SIMD (MI355X: 256 CUs x 4 SIMDs)
 static uint32_t miller_round_lanes() {
@@ -179,14 +274,19 @@ static uint32_t miller_round_lanes() {
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
+  if (bgv_sig_pairs(b)) {  // no group sums: every slot's own signature pair beside its set pair
+    hipLaunchKernelGGL(k_miller_wide, dim3(2 * n), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
+                       b.pk_status, b.f, n, b.gsum, b.gpair, b.rsig, b.fsig);
+    BGV_MARK(3);
+    return hipGetLastError();
+  }
   // the groups' signature sums, then set pairs and group pairs in one launch
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
                      b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum);
   BGV_MARK(2);
   const uint32_t R = miller_round_lanes();
   if (bgv_use_latency(b, n + b.ngroups)) {
-    hipLaunchKernelGGL(k_miller_team, dim3(nblk(n + b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, n,
-                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+    launch_miller_latency(b, n, b.ngroups, s.main);
   } else if (b.path != BGV_PATH_BULK && b.ngroups <= bgv_latency_max() &&
              (n + b.ngroups + R - 1) / R > (n + R - 1) / R) {
     // the group pairs on extra k_miller lanes would open one more round of one wave per SIMD
@@ -214,8 +314,7 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum);
   if (b.ngroups <= bgv_latency_max())
-    hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u, b.rpk,
-                       b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+    launch_miller_latency(b, 0u, b.ngroups, st);
   else
     hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);
   return hipGetLastError();

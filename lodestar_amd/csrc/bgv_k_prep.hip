@@ -14,6 +14,7 @@
 #include "bgv_k_tasks.h"
 #include "bgv_team_dev.h"
 #include "bgv_tcurve.h"
+#include "bgv_tround_dev.h"
 
 static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
 
@@ -54,6 +55,10 @@ struct tc_dev_engine {
   }
 };
 
+#ifndef BGV_WPE_AGG
+#define BGV_WPE_AGG 2
+#endif
+
 extern "C" {
 
 
@@ -63,11 +68,9 @@ extern "C" {
 // partial sum (lane ^ 32, 16, ..., 1) exchanged in registers.  Every lane ends with the
 // total; the sum is the same group element as the serial one.  Waves of slots with fewer
 // than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane reads the same slot).
-__global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                               const uint32_t* __restrict__ pk_idx,
-                                               const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
-  const uint32_t s = blockIdx.x;
-  if (s >= nslots) return;
+__device__ __forceinline__ void pk_aggw_body(const bgv_dslot* __restrict__ slots, uint32_t s,
+                                             const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                             g1_jac* __restrict__ pk_agg) {
   const bgv_dslot& d = slots[s];
   if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk <= BGV_PK_TEAM_MAX) return;
   const uint32_t l = threadIdx.x;
@@ -80,6 +83,42 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   acc = jac_add(acc, point_xor<2>(acc));
   acc = jac_add(acc, point_xor<1>(acc));
   if (l == 0) pk_agg[s] = acc;
+}
+
+__device__ __forceinline__ void pk_agg16_body(const bgv_dslot* __restrict__ slots, uint32_t nslots, uint32_t blk,
+                                              const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                              g1_jac* __restrict__ pk_agg) {
+  const uint32_t s = blk * (64 / 16) + threadIdx.x / 16;
+  const uint32_t l = threadIdx.x % 16;
+  const bgv_dslot* d = s < nslots ? &slots[s] : nullptr;
+  const bool act = d && !(d->flags & BGV_SLOT_PAD) && (d->flags & BGV_SLOT_PK_CACHED) &&
+                   d->n_pk >= BGV_PK_TREE_MIN && d->n_pk <= BGV_PK_TEAM_MAX;
+  g1_jac acc = jac_infinity<fp_t>();
+  if (act) {  // n_pk >= 16: every lane has a first key
+    const uint32_t* idx = pk_idx + d->pk_off;
+    const uint32_t n = d->n_pk;
+    acc = jac_from_aff(cache[idx[l]]);
+    uint32_t k = l + 16;
+    g1_aff cur = cache[idx[k < n ? k : l]];
+    for (; k < n; k += 16) {
+      const uint32_t kn = k + 16 < n ? k + 16 : k;
+      const g1_aff nxt = cache[idx[kn]];
+      acc = jac_add_aff(acc, cur);
+      cur = nxt;
+    }
+  }
+  // every lane of the wave reaches the exchanges
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (act && l == 0) pk_agg[s] = acc;
+}
+
+__global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                               const uint32_t* __restrict__ pk_idx,
+                                               const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
+  if (blockIdx.x < nslots) pk_aggw_body(slots, blockIdx.x, pk_idx, cache, pk_agg);
 }
 
 // ---- latency path ------------------------------------------------------------------------
@@ -127,11 +166,24 @@ __device__ __noinline__ void task_sig_decode(uint32_t s, const bgv_dslot* __rest
   sig_status[s] = st;
 }
 
+// merged (the smallest calls, with k_prep_wide): plane 3 sums committee-sized sets' cached
+// keys (k_pk_agg16's teams), plane 4 larger sets' (k_pk_agg's wave tree), and k_prep_wide
+// does the pubkey task after them; the key trees then overlap the hash and decode planes
+// instead of running before them.  Otherwise plane 3 is the pubkey task.
 __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
                                         fp12_t* __restrict__ f, int32_t* __restrict__ sig_status,
                                         const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                         const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                        int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg) {
+                                        int32_t* __restrict__ pk_status, g1_jac* __restrict__ pk_agg, int merged) {
+  if (merged && blockIdx.y >= 3) {  // block-uniform
+    if (!pk_agg) return;
+    if (blockIdx.y == 3) {
+      if (blockIdx.x < (nslots + 3) / 4) pk_agg16_body(slots, nslots, blockIdx.x, pk_idx, cache, pk_agg);
+    } else if (blockIdx.x < nslots) {
+      pk_aggw_body(slots, blockIdx.x, pk_idx, cache, pk_agg);
+    }
+    return;
+  }
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   if (blockIdx.y == 0)
@@ -207,43 +259,127 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
   }
 }
 
+// The point-program engine of bgv_tcurve.h's schedules on a whole block (bgv_tround_dev.h:
+// four-part round instructions): bank moves by the q = 0 lanes, one block per set.
+struct tc_wide_engine : tr_wide_engine {
+  __device__ void copy(int dst, int src) {
+    if (q == 0 && c < 6 && dst != src) S[TCP_BANK(dst) + c] = S[TCP_BANK(src) + c];
+    __syncthreads();
+  }
+  __device__ void neg_y(int b) {
+    if (q == 0 && (c == 2 || c == 3)) S[TCP_BANK(b) + c] = fp_neg(S[TCP_BANK(b) + c]);
+    __syncthreads();
+  }
+  __device__ void check_add() {
+    if (q == 0 && c == 0) {
+      const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
+      bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+    }
+  }
+};
+
+// k_prep_team for the smallest calls, one set per 64-lane block and task (blockIdx.y): 0 the
+// cofactor clearing of q0 + q1, 1 r_i * sig_i, 2 the signature's subgroup check psi(P) ==
+// [x]P with [|x|]P from the same point programs (a team-level exceptional addition falls
+// back to the one-lane g2_in_subgroup).  Same schedules and formulas as k_prep_team.
+__global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                  g2_jac* __restrict__ h, fp12_t* __restrict__ f,
+                                                  g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status,
+                                                  const uint32_t* __restrict__ pk_idx,
+                                                  const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
+                                                  g1_jac* __restrict__ rpk, int32_t* __restrict__ pk_status,
+                                                  const g1_jac* __restrict__ pk_agg) {
+  __shared__ uint8_t prog[TCP_TABLE_BYTES];
+  __shared__ fp_t S[TCP_NSLOT];
+  __shared__ fp_t RP[64];
+  __shared__ int flag;
+  if (blockIdx.y == 3) {  // the pubkey task of the merged k_prep_a, one lane per set
+    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+    if (s < nslots) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+    return;
+  }
+  const uint32_t uu = blockIdx.x;  // grid = exactly nslots blocks per task
+  const int lane = threadIdx.x, c = lane % BGV_TEAM, q = lane / BGV_TEAM;
+  const bgv_dslot& d = slots[uu];
+  const bool real = !(d.flags & BGV_SLOT_PAD);
+  // the subgroup check only for signatures that decoded to a finite point (uniform per block)
+  if (blockIdx.y == 2 && (!real || sig_status[uu] != BGV_ST_OK)) return;
+  for (int i = lane; i < TCP_TABLE_BYTES; i += 64) prog[i] = kTcProg[i];
+  if (q == 0) {
+    if (c == 6) {
+      S[TCP_S_ONE] = fp_one();
+    } else if (c >= 7 && c < 11) {
+      const fp2_t cx = BGV_PSI_CX, cy = BGV_PSI_CY;
+      const fp2_t& v = c < 9 ? cx : cy;
+      S[c < 9 ? TCP_S_PSI_CX + (c - 7) : TCP_S_PSI_CY + (c - 9)] = (c & 1) ? v.c0 : v.c1;
+    } else if (c == 11) {
+      S[TCP_S_PSI2_CX] = fp_t{BGV_PSI2_CX};
+    } else if (c == 12) {
+      S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
+    }
+  }
+  tc_wide_engine e{{prog, S, RP, c, q, false}};
+  if (blockIdx.y == 0) {
+    if (q == 0 && c < 6) {
+      S[TCP_BANK(1) + c] = reinterpret_cast<const fp_t*>(h + uu)[c];
+      S[TCP_BANK(2) + c] = reinterpret_cast<const fp_t*>(split_q1(f, uu))[c];
+    }
+    __syncthreads();
+    tc_clear_cofactor(e);
+    if (lane == 0) flag = e.bad ? 1 : 0;
+    __syncthreads();
+    if (real) {
+      if (!flag) {
+        if (q == 0 && c < 6) reinterpret_cast<fp_t*>(h + uu)[c] = S[TCP_BANK(3) + c];
+      } else if (lane == 0) {
+        h[uu] = g2_clear_cofactor(jac_add(h[uu], *split_q1(f, uu)));
+      }
+    }
+  } else if (blockIdx.y == 1) {
+    const bool ok = sig_status[uu] == BGV_ST_OK;  // read before the subgroup blocks may flip it
+    if (q == 0) {
+      if (c < 4)
+        S[TCP_BANK(1) + c] = reinterpret_cast<const fp_t*>(split_sig(f, uu))[c];
+      else if (c < 6)
+        S[TCP_BANK(1) + c] = c == 4 ? fp_one() : fp_zero();
+    }
+    __syncthreads();
+    tc_mul_glv(e, d.scalar);
+    if (real && ok && q == 0 && c < 6) reinterpret_cast<fp_t*>(rsig + uu)[c] = S[TCP_BANK(4) + c];
+  } else {
+    // [|x|]P: base in bank 0, the accumulator (= P) in bank 4
+    if (q == 0 && c < 6) {
+      const fp_t v = c < 4 ? reinterpret_cast<const fp_t*>(split_sig(f, uu))[c] : (c == 4 ? fp_one() : fp_zero());
+      S[TCP_BANK(0) + c] = v;
+      S[TCP_BANK(4) + c] = v;
+    }
+    __syncthreads();
+    const int a = tc_mul_x_abs(e);
+    if (lane == 0) {
+      const g2_jac p = jac_from_aff(*split_sig(f, uu));
+      bool in;
+      if (e.bad) {
+        in = g2_in_subgroup(p);
+      } else {
+        const fp_t* B = S + TCP_BANK(a);
+        const g2_jac xp = {{B[0], B[1]}, {B[2], B[3]}, {B[4], B[5]}};
+        in = jac_eq(g2_psi(p), jac_neg(xp));  // psi(P) == [x]P = -[|x|]P
+      }
+      if (!in) sig_status[uu] = BGV_POINT_NOT_IN_GROUP;
+    }
+  }
+}
+
 // Committee-sized sets (BGV_PK_TREE_MIN..BGV_PK_TEAM_MAX cached keys, e.g. 128-key
 // attestation aggregates) on a team of 16 lanes, four sets per wave: lane l sums keys
 // l, l + 16, ... with mixed additions, then four ds_swizzle butterfly levels (xor 8..1, inside
 // the team).  A whole wave per 128-key set spent ~4x the lane work on the tree levels.
 // The lane's first key starts the sum (no addition to infinity), and each key is gathered
 // one addition ahead of its use.  A gather-latency-bound kernel: BGV_WPE_AGG waves per SIMD.
-#ifndef BGV_WPE_AGG
-#define BGV_WPE_AGG 2
-#endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_AGG, BGV_WPE_AGG)))
 k_pk_agg16(const bgv_dslot* __restrict__ slots, uint32_t nslots, const uint32_t* __restrict__ pk_idx,
            const g1_aff* __restrict__ cache, g1_jac* __restrict__ pk_agg) {
-  const uint32_t s = blockIdx.x * (64 / 16) + threadIdx.x / 16;
-  const uint32_t l = threadIdx.x % 16;
-  const bgv_dslot* d = s < nslots ? &slots[s] : nullptr;
-  const bool act = d && !(d->flags & BGV_SLOT_PAD) && (d->flags & BGV_SLOT_PK_CACHED) &&
-                   d->n_pk >= BGV_PK_TREE_MIN && d->n_pk <= BGV_PK_TEAM_MAX;
-  g1_jac acc = jac_infinity<fp_t>();
-  if (act) {  // n_pk >= 16: every lane has a first key
-    const uint32_t* idx = pk_idx + d->pk_off;
-    const uint32_t n = d->n_pk;
-    acc = jac_from_aff(cache[idx[l]]);
-    uint32_t k = l + 16;
-    g1_aff cur = cache[idx[k < n ? k : l]];
-    for (; k < n; k += 16) {
-      const uint32_t kn = k + 16 < n ? k + 16 : k;
-      const g1_aff nxt = cache[idx[kn]];
-      acc = jac_add_aff(acc, cur);
-      cur = nxt;
-    }
-  }
-  // every lane of the wave reaches the exchanges
-  acc = jac_add(acc, point_xor<8>(acc));
-  acc = jac_add(acc, point_xor<4>(acc));
-  acc = jac_add(acc, point_xor<2>(acc));
-  acc = jac_add(acc, point_xor<1>(acc));
-  if (act && l == 0) pk_agg[s] = acc;
+  pk_agg16_body(slots, nslots, blockIdx.x, pk_idx, cache, pk_agg);
 }
 
 // PublicKey.aggregate(...).toBytes(uncompressed) over cached keys through the verify
@@ -270,6 +406,16 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   BGV_MARK(0);
   // k_pk_agg only when some set is large enough; otherwise k_prep sums serially (null pk_agg)
   const bool tree = b.max_npk >= BGV_PK_TREE_MIN;
+  const bool wide = bgv_use_latency(b, n + b.ngroups) && n <= BGV_PREP_WIDE_MAX;
+  if (wide) {
+    const g1_aff* cache = reinterpret_cast<const g1_aff*>(b.cache_opaque);
+    hipLaunchKernelGGL(k_prep_a, dim3(n, 5), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status, b.pk_idx,
+                       cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr, 1);
+    hipLaunchKernelGGL(k_prep_wide, dim3(n, 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
+                       b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
+    BGV_MARK(1);
+    return hipGetLastError();
+  }
   if (tree)
     hipLaunchKernelGGL(k_pk_agg16, dim3(nblk(n, 4)), dim3(64), 0, s.main, b.slots, n, b.pk_idx,
                        reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_agg);
@@ -279,7 +425,7 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   if (bgv_use_latency(b, n + b.ngroups)) {
     hipLaunchKernelGGL(k_prep_a, dim3(nblk(n, 64), 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                       tree ? b.pk_agg : nullptr);
+                       tree ? b.pk_agg : nullptr, 0);
     hipLaunchKernelGGL(k_prep_team, dim3(nblk(n, BGV_FINAL_TEAMS), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f,
                        b.rsig, b.sig_status);
   } else {

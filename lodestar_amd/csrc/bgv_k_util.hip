@@ -198,7 +198,7 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 }  // extern "C"
 
 size_t bgv_slot_bytes() {
-  return 2 * sizeof(g2_jac) + sizeof(g1_jac) + sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t);
+  return 2 * sizeof(g2_jac) + sizeof(g1_jac) + 2 * sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t);
 }
 size_t bgv_group_bytes() { return sizeof(g2_jac) + 3 * sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
@@ -212,6 +212,8 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   b->rpk = reinterpret_cast<g1_jac*>(p);
   p += sizeof(g1_jac) * (size_t)cap_slots;
   b->f = reinterpret_cast<fp12_t*>(p);
+  p += sizeof(fp12_t) * (size_t)cap_slots;
+  b->fsig = reinterpret_cast<fp12_t*>(p);
   p += sizeof(fp12_t) * (size_t)cap_slots;
   b->pk_agg = reinterpret_cast<g1_jac*>(p);
   p += sizeof(g1_jac) * (size_t)cap_slots;

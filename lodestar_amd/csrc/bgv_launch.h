@@ -43,6 +43,7 @@ struct bgv_dev_batch {
   jac_t<fp2_t>* h;     // H(m_i), Jacobian
   jac_t<fp_t>* rpk;    // r_i * aggregated pubkey, Jacobian
   fp12_t* f;           // per-slot Miller loop value e(r_i pk_i, H(m_i))
+  fp12_t* fsig;        // smallest calls' first pass: per-slot e(-G1, r_i sig_i) (bgv_sig_pairs)
   jac_t<fp_t>* pk_agg;  // wavefront-tree sum of a many-key set's cached pubkeys (k_pk_agg)
   int32_t* sig_status;
   int32_t* pk_status;
@@ -68,6 +69,11 @@ struct bgv_streams {
   hipEvent_t* kev;  // 2 * BGV_NKERNELS events (start/end per kernel) or nullptr
 };
 hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // prep + miller
+// The smallest calls' first pass pairs every signature with -G1 on its own (e(-G1, r_i sig_i)
+// per slot, beside e(r_i pk_i, H(m_i))) instead of summing a group's r_i sig_i first (k_gsum)
+// and pairing the sum: one more Miller loop per set, run in parallel, for one serial kernel
+// less.  Retry rounds keep the group sums.
+bool bgv_sig_pairs(const bgv_dev_batch& b);
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree);  // bgv_k_prep_bulk.hip
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);

@@ -62,4 +62,56 @@ struct tm_dev_ops_t {
 };
 using tm_dev_ops = tm_dev_ops_t<BGV_TEAM>;
 
+// One Fp12 value per 64-lane block with the wide products (bls_team.h tm_mul_part): lane l
+// holds coefficient c = l % 12 (replicated over q = l / 12); lanes q < 4 (l < 48) each compute
+// a quarter of the double-width products of their coefficient, lanes 48..63 only keep the
+// barriers.  A: 12 operand slots, B: 12, P: 4 x 12 part slots (LDS).
+struct tm_wide_ops {
+  fp_t* A;
+  fp_t* B;
+  fp_t* P;
+  int c, q;
+  __device__ fp_t gather() {
+    return tm_sum4(P[c], P[BGV_TEAM_COMPS + c], P[2 * BGV_TEAM_COMPS + c], P[3 * BGV_TEAM_COMPS + c]);
+  }
+  __device__ fp_t mul(const fp_t& x, const fp_t& y) {
+    if (q == 0) {
+      A[c] = x;
+      B[c] = y;
+    }
+    __syncthreads();
+    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_part(c, q, A, B);
+    __syncthreads();
+    return gather();
+  }
+  __device__ fp_t sqr(const fp_t& x) {
+    if (q == 0) A[c] = x;
+    __syncthreads();
+    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_sqr_part(c, q, A);
+    __syncthreads();
+    return gather();
+  }
+  __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    if (q == 0) A[c] = x;
+    __syncthreads();
+    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_line_part(c, q, A, l0, l1, l3);
+    __syncthreads();
+    return gather();
+  }
+  __device__ fp_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) { return tm_line_lane(c, l0, l1, l3); }
+  __device__ fp_t conj(const fp_t& x) { return fp_select(((c >> 1) & 1) != 0, x, fp_neg(x)); }
+  __device__ fp_t frob(const fp_t& x) {
+    if (q == 0) A[c] = x;
+    __syncthreads();
+    const fp_t x0 = A[c & ~1], x1 = A[c | 1];
+    __syncthreads();
+    return tm_frob_lane(c, x0, x1, kTeamFrob1[tm_tower_pos(c)]);
+  }
+  __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(c)]); }
+  __device__ bool is_fp6(const fp_t& x) {
+    const bool bad = q == 0 && ((c >> 1) & 1) && !fp_is_zero(x);
+    return __ballot(bad) == 0;  // the whole block holds one value
+  }
+};
+
 

@@ -133,6 +133,111 @@ BGV_HD fp_t tm_sqr_lane(int c, const fp_t* A) {
   return wide_redc(t);
 }
 
+// Wide products (the latency path's final exponentiation): coefficient c is split over four
+// lanes q = 0..3, each accumulating part of its double-width products and reducing them
+// (REDC is linear, so the four results sum to the coefficient mod p).  A product then costs a
+// lane 4 double-width products + 1 reduction instead of 12 + 1, a squaring 2 + 1 instead of
+// 7 + 1.  Parts of tm_mul_lane's six i-terms: q0 {0, 4}, q1 {1, 5}, q2 {2}, q3 {3}; of
+// tm_sqr_lane's three pairs and the diagonal: one each.  Each part is < 2p (few products).
+BGV_HD fp_t tm_mul_part(int c, int q, const fp_t* A, const fp_t* B) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  BGV_UNROLL for (int r = 0; r < 2; ++r) {
+    const int i = q + 4 * r;
+    const bool live = i < 6;
+    const int ii = live ? i : 0;
+    const bool wrap = ii > k;
+    const int j = wrap ? k + 6 - ii : k - ii;
+    const fp_t x0 = A[2 * ii], x1 = A[2 * ii + 1];
+    const fp_t y0 = B[2 * j], y1 = B[2 * j + 1];
+    const fp_t d = fp_sub_nr(y0, y1);
+    const fp_t s = fp_add_norm(y0, y1);
+    const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+    const fp_t X2 = fp_select(e != 0, x1n, x1);
+    const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+    const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+    const fp_t z = fp_zero();
+    wide_mac(t, live ? x0 : z, Y1);  // the second term of q2 / q3 multiplies zeros
+    wide_mac(t, live ? X2 : z, Y2);
+  }
+  return wide_redc(t);
+}
+
+BGV_HD fp_t tm_sqr_part(int c, int q, const fp_t* A) {
+  const int k = c >> 1, e = c & 1;
+  const uint32_t kI[6] = {0x321, 0x320, 0x430, 0x410, 0x510, 0x210};
+  const uint32_t kJ[6] = {0x345, 0x451, 0x452, 0x523, 0x534, 0x345};
+  const uint32_t kW[6] = {0x7, 0x6, 0x6, 0x4, 0x4, 0x0};
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  const int p = q < 3 ? q : 0;
+  const int i = (kI[k] >> (4 * p)) & 0xf, j = (kJ[k] >> (4 * p)) & 0xf;
+  const bool wrap = (kW[k] >> p) & 1;
+  const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+  const fp_t y0 = A[2 * j], y1 = A[2 * j + 1];
+  const fp_t d = fp_sub_nr(y0, y1);
+  const fp_t s = fp_add_norm(y0, y1);
+  const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+  const fp_t X2n = fp_select(e != 0, x1n, x1);
+  const bool cross = i != j;
+  const fp_t X1 = fp_select(cross, x0, fp_add_norm(x0, x0));
+  const fp_t X2 = fp_select(cross, X2n, fp_add_norm(X2n, X2n));
+  const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+  const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+  // q3: the unwrapped diagonal (even k) as in tm_sqr_lane, zero for odd k
+  const int h = k >> 1;
+  const fp_t h0 = A[2 * h], h1 = A[2 * h + 1];
+  const bool diag = q == 3, even = (k & 1) == 0;
+  const fp_t P = e ? fp_add_norm(h0, h0) : fp_add_norm(h0, h1);
+  const fp_t Q = e ? h1 : fp_sub_nr(h0, h1);
+  const fp_t z = fp_zero();
+  wide_mac(t, diag ? (even ? P : z) : X1, diag ? Q : Y1);
+  wide_mac(t, diag ? z : X2, Y2);
+  return wide_redc(t);
+}
+
+// tm_mul_line_lane split the same way: the three line terms on parts 0..2, part 3 adds 0
+BGV_HD fp_t tm_mul_line_part(int c, int q, const fp_t* A, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  const int term = q < 3 ? q : 0;
+  const int j = term == 0 ? 0 : term + 1;  // 0, 2, 3
+  const fp2_t& y = term == 0 ? l0 : (term == 1 ? l1 : l3);
+  const bool wrap = k < j;
+  const int i = wrap ? k - j + 6 : k - j;
+  const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+  const fp_t d = fp_sub_nr(y.c0, y.c1);
+  const fp_t s = fp_add_norm(y.c0, y.c1);
+  const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+  const fp_t X2 = fp_select(e != 0, x1n, x1);
+  const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y.c0, y.c1);
+  const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y.c1, y.c0);
+  const fp_t z = fp_zero();
+  wide_mac(t, q < 3 ? x0 : z, Y1);
+  wide_mac(t, q < 3 ? X2 : z, Y2);
+  return wide_redc(t);
+}
+
+// sum of the four parts of a coefficient, back below 2p
+BGV_HD fp_t tm_sum4(const fp_t& a, const fp_t& b, const fp_t& c, const fp_t& d) {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i] + c.v[i] + d.v[i];
+  // value < 8p, limbs < 2^30: one signed chain subtracting q p, q from the top limb (lz_out)
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  const uint32_t qt = r.v[NL - 1] / (uint32_t)(P_[NL - 1] + 1);
+  int64_t cy = 0;
+  fp_t o;
+  BGV_UNROLL for (int i = 0; i < NL - 1; ++i) {
+    const int64_t s = (int64_t)r.v[i] - (int64_t)((uint64_t)qt * P_[i]) + cy;
+    o.v[i] = (uint32_t)s & LMASK;
+    cy = s >> LBITS;
+  }
+  o.v[NL - 1] = (uint32_t)((int64_t)r.v[NL - 1] - (int64_t)((uint64_t)qt * P_[NL - 1]) + cy);
+  return o;
+}
+
 // Frobenius (p-power) on the component pair (x0, x1) = f_k:
 // frob(f)_k = conj(f_k) * g_k, g = BGV_FROB1 indexed by tower position.
 BGV_HD fp_t tm_frob_lane(int c, const fp_t& x0, const fp_t& x1, const fp2_t& g) {
@@ -299,6 +404,30 @@ struct tm_emu_ops {
     for (int c = 0; c < BGV_TEAM_COMPS; ++c)
       if ((c >> 1) & 1) z = z && fp_is_zero(a.c[c]);
     return z;
+  }
+};
+
+// the wide products (four parts per coefficient, tm_mul_part / tm_sqr_part), lane by lane
+struct tm_emu_wide_ops : tm_emu_ops {
+  BGV_HD tm_emu_t mul(const tm_emu_t& a, const tm_emu_t& b) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      r.c[c] = tm_sum4(tm_mul_part(c, 0, a.c, b.c), tm_mul_part(c, 1, a.c, b.c), tm_mul_part(c, 2, a.c, b.c),
+                       tm_mul_part(c, 3, a.c, b.c));
+    return r;
+  }
+  BGV_HD tm_emu_t sqr(const tm_emu_t& a) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      r.c[c] = tm_sum4(tm_sqr_part(c, 0, a.c), tm_sqr_part(c, 1, a.c), tm_sqr_part(c, 2, a.c), tm_sqr_part(c, 3, a.c));
+    return r;
+  }
+  BGV_HD tm_emu_t mul_line(const tm_emu_t& a, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+      r.c[c] = tm_sum4(tm_mul_line_part(c, 0, a.c, l0, l1, l3), tm_mul_line_part(c, 1, a.c, l0, l1, l3),
+                       tm_mul_line_part(c, 2, a.c, l0, l1, l3), tm_mul_line_part(c, 3, a.c, l0, l1, l3));
+    return r;
   }
 };
 

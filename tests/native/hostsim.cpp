@@ -220,6 +220,19 @@ int hs_team_final_is_one(const uint8_t* f) {
   return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
 }
 int hs_final_is_one(const uint8_t* f) { return fp12_is_one(final_exp(in_fp12(f))); }
+// the wide (four parts per coefficient) products of the latency path's closing
+void hs_team_mul_wide(uint8_t* r, const uint8_t* a, const uint8_t* b) {
+  tm_emu_wide_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul(tm_emu_from_fp12(in_fp12(a)), tm_emu_from_fp12(in_fp12(b)))));
+}
+void hs_team_sqr_wide(uint8_t* r, const uint8_t* a) {
+  tm_emu_wide_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.sqr(tm_emu_from_fp12(in_fp12(a)))));
+}
+int hs_team_final_is_one_wide(const uint8_t* f) {
+  tm_emu_wide_ops o;
+  return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
+}
 // Q handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
 static g2_jac jac_scaled(const g2_aff& a) {
   const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};
@@ -265,8 +278,20 @@ int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
 void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
   out_fp12(out, tm_team_miller_host(g1_scaled(in_g1(p)), jac_scaled(in_g2(q))));
 }
+// k_miller_wide: four-part round instructions and the wide Fp12 products
+void hs_tmiller_wide(uint8_t* out, const uint8_t* p, const uint8_t* q) {
+  tmp_host_wide() = true;
+  out_fp12(out, tm_team_miller_host<tm_emu_wide_ops>(g1_scaled(in_g1(p)), jac_scaled(in_g2(q))));
+  tmp_host_wide() = false;
+}
+// the point programs' rounds as four-part instructions (k_prep_wide) from now on, or not
+void hs_set_wide_rounds(int on) { tmp_host_wide() = on != 0; }
 void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   tm_emu_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul_line(tm_emu_from_fp12(in_fp12(f)), in_fp2(l0), in_fp2(l1), in_fp2(l3))));
+}
+void hs_team_mul_line_wide(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
+  tm_emu_wide_ops o;
   out_fp12(r, tm_emu_to_fp12(o.mul_line(tm_emu_from_fp12(in_fp12(f)), in_fp2(l0), in_fp2(l1), in_fp2(l3))));
 }
 // one set through the device equation: k_prep (r pk affine, r sig Jacobian), k_miller

@@ -324,6 +324,8 @@ def test_table_driven_team_miller_loop(L):
         L.hs_miller_loop1(m1, hs.g1_b(p), hs.g2_b(q))
         L.hs_tmiller(tm, hs.g1_b(p), hs.g2_b(q))
         assert tm.raw == m1.raw
+        L.hs_tmiller_wide(tm, hs.g1_b(p), hs.g2_b(q))  # k_miller_wide: four-part instructions
+        assert tm.raw == m1.raw
 
 
 def test_team_g2_schedules(L):
@@ -331,12 +333,17 @@ def test_team_g2_schedules(L):
     programs, emulated lane by lane) equal g2_clear_cofactor and jac_mul_glv as points, for
     random messages and randomizer words (including zero top digits and a word of 1)."""
     import ctypes
-    for k, m in enumerate((b"a", b"tcurve", b"x" * 7)):
-        msg = hashlib.sha256(m).digest()
-        scalar = (rnd.getrandbits(64) | 1) if k == 0 else (1 if k == 1 else rnd.getrandbits(40) | 1)
-        bad = ctypes.c_int(7)
-        assert L.hs_tcurve_check(msg, ctypes.c_uint64(scalar), ctypes.byref(bad)) == 1
-        assert bad.value == 0
+    for wide in (0, 1):  # 1: the rounds as four-part instructions (k_prep_wide)
+        L.hs_set_wide_rounds(wide)
+        try:
+            for k, m in enumerate((b"a", b"tcurve", b"x" * 7)):
+                msg = hashlib.sha256(m).digest()
+                scalar = (rnd.getrandbits(64) | 1) if k == 0 else (1 if k == 1 else rnd.getrandbits(40) | 1)
+                bad = ctypes.c_int(7)
+                assert L.hs_tcurve_check(msg, ctypes.c_uint64(scalar), ctypes.byref(bad)) == 1
+                assert bad.value == 0
+        finally:
+            L.hs_set_wide_rounds(0)
 
 
 def test_team_mul_line(L):
@@ -347,6 +354,8 @@ def test_team_mul_line(L):
         want, got = hs.buf(576), hs.buf(576)
         L.hs_fp12_mul_line(want, f, l0, l1, l3)
         L.hs_team_mul_line(got, f, l0, l1, l3)
+        assert got.raw == want.raw
+        L.hs_team_mul_line_wide(got, f, l0, l1, l3)  # four parts per coefficient (k_miller_wide)
         assert got.raw == want.raw
 
 
@@ -377,8 +386,12 @@ def test_team_fp12_ops(L):
         L.hs_fp12_mul(want, a, b)
         L.hs_team_mul(got, a, b)
         assert got.raw == want.raw
+        L.hs_team_mul_wide(got, a, b)  # four parts per coefficient (latency-path closing)
+        assert got.raw == want.raw
         L.hs_fp12_sqr(want, a)
         L.hs_team_sqr(got, a)  # 7-product team squaring
+        assert got.raw == want.raw
+        L.hs_team_sqr_wide(got, a)
         assert got.raw == want.raw
         for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
             tf(got, a)
@@ -395,6 +408,7 @@ def test_team_final_exp_check(L):
         f = rf12()
         assert L.hs_final_is_one(f) == 0
         assert L.hs_team_final_is_one(f) == 0
+        assert L.hs_team_final_is_one_wide(f) == 0
     p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
     q = g2_rand_in_group()
     # e(P, Q) e(-P, Q) == 1 and e(P, Q) e(-P, Q2) != 1 (Miller values multiplied)
@@ -404,8 +418,10 @@ def test_team_final_exp_check(L):
     L.hs_fp12_mul(m, a.raw, b.raw)
     assert L.hs_final_is_one(m.raw) == 1
     assert L.hs_team_final_is_one(m.raw) == 1
+    assert L.hs_team_final_is_one_wide(m.raw) == 1
     q2 = g2_rand_in_group()
     L.hs_miller_loop(b, hs.g1_b(o.g1_neg(p)), hs.g2_b(q2))
     L.hs_fp12_mul(m, a.raw, b.raw)
     assert L.hs_final_is_one(m.raw) == 0
     assert L.hs_team_final_is_one(m.raw) == 0
+    assert L.hs_team_final_is_one_wide(m.raw) == 0
