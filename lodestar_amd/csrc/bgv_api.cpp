@@ -30,6 +30,7 @@
 #include <condition_variable>
 #include <unordered_map>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <thread>
@@ -37,7 +38,7 @@
 
 #include "../../include/blsgpu.h"
 #include "bgv_launch.h"
-#include "bls_field.h"  // host Fp12 product of the retry rounds' complement checks
+#include "bls_field.h"  // fp12_t (sizes of the per-group u copies)
 
 // parts a failing mixed group is split into per retry round (BGV_RETRY_FANOUT env).
 // Group closings are team-parallel and cheap in latency, so bisecting (64 -> 8 -> 1)
@@ -92,6 +93,12 @@ static int dispatchers_per_device() {
   static const int v = (int)env_size("BGV_DISPATCHERS", BGV_DISPATCHERS, 1);
   return v;
 }
+// Exec buffer sets per device (BGV_EXECS): one per dispatcher plus the ones whose super-batch
+// is in its retry rounds
+static int execs_per_device() {
+  static const int v = (int)env_size("BGV_EXECS", 2 * BGV_DISPATCHERS, 1);
+  return std::max(v, dispatchers_per_device());
+}
 
 extern "C" int bgv_device_count(void) {
   int n = 0;
@@ -128,8 +135,10 @@ struct Pinned {
 
 // One dispatcher's device resources: its stream, events and buffers.
 struct Exec {
-  hipStream_t main = nullptr;   // per-set kernels (compute-bound)
-  hipStream_t close = nullptr;  // group closing + retry rounds (latency-bound): high priority
+  // streams lent by the user of the buffers: the dispatcher's stream for a super-batch's first
+  // pass, the device's retry stream for its retry rounds (Device::sched)
+  hipStream_t main = nullptr;   // per-set kernels and the first pass's closing
+  hipStream_t close = nullptr;  // retry rounds (latency-bound): high priority
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_prep = nullptr, ev_sets = nullptr;
   hipEvent_t kev[2 * BGV_NKERNELS] = {};
   void* slot_mem = nullptr;
@@ -167,8 +176,43 @@ struct FinalScratch {
   size_t cap = 0;
 };
 
+struct Call;
+// What a super-batch's retry rounds need from its first pass.
+struct BatchState {
+  std::chrono::steady_clock::time_point tb;
+  double t_merge = 0, t_tok = 0, t_sets = 0, t_pass1 = 0, t_post = 0;
+  uint32_t nslots = 0, ngroups = 0;
+  std::vector<uint32_t> call_gb;  // each call's first group in the merged batch
+  bool want_gu = false;           // the first pass's u values are in x.d_gu1 (pattern tests)
+  bool prof = false;
+};
+// A super-batch whose first pass is done and whose retry rounds wait for the retry thread.
+struct RetryJob {
+  std::vector<Call*> calls;
+  Exec* x = nullptr;
+  std::shared_ptr<BatchState> st;
+};
+// Exec buffer sets and retry rounds of one device.  A dispatcher takes a free Exec for each
+// super-batch and, when its first pass leaves failing groups, hands the batch to the device's
+// retry thread and goes on with the next super-batch; the Exec returns to the pool when the
+// retry rounds are done.  So the latency-bound retry rounds of one batch overlap the per-set
+// kernels of the next ones instead of holding a dispatcher.  Streams: one per dispatcher, one
+// (high priority) for the retry rounds, the utility stream: within the device's 4 hardware
+// queues (GPU_MAX_HW_QUEUES).
+struct DevSched {
+  std::mutex mu;
+  std::condition_variable cv;  // an Exec was released / a retry job was queued / stop
+  std::deque<Exec*> free;
+  std::deque<RetryJob> rq;
+  bool stop = false;
+  std::thread retry_thread;
+  hipStream_t retry = nullptr;
+  std::vector<hipStream_t> dstreams;
+};
+
 struct Device {
   int id = 0;
+  std::unique_ptr<DevSched> sched = std::make_unique<DevSched>();
   FinalScratch final_scratch;
   hipStream_t stream = nullptr;      // utility work (cache upload, hooks, keygen)
   bgv_cache_entry* cache = nullptr;  // pubkey cache (replicated on every device)
@@ -286,10 +330,20 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // group is resolved in at most two rounds: a round costs about the same latency whether it
 // tests hundreds or thousands of groups, while a second pattern round over the candidates
 // need not shrink them (two invalid jobs at the first and last candidate index).
+//
+// Two invalid jobs i, j (the usual case of a second round) leave as candidates the 2^h jobs
+// that agree with both where i and j agree, h = the number of bits D where S_b and its
+// complement both failed; the candidates pair up as x, x ^ D.  The next round tests the pairs
+// (2^(h-1) tests instead of 2^h single jobs): when exactly one test fails and it is a pair,
+// both its jobs are invalid (for b in D, S_b and its complement each hold an invalid job, and
+// every invalid job is a candidate of that one pair); a failing single job is invalid; jobs of
+// a failing pair next to other failures are tested alone in one more round.
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
-  std::vector<size_t> jobs;        // its jobs in slot order
-  std::vector<uint32_t> tests;     // round group index of S_j
+  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs
+  std::vector<size_t> jobs;        // kind 0: its jobs in slot order
+  std::vector<uint32_t> tests;     // round group index of each test
+  std::vector<std::vector<size_t>> test_jobs;  // kind 1: each test's jobs
 };
 // units from the first pass of at most this many jobs (not pattern-testable) are tested one
 // job per device group
@@ -316,6 +370,8 @@ struct Call {
   std::vector<std::vector<size_t>> units;  // pending retry units
   std::vector<int> unit_group;             // first-pass group the unit's jobs lie in (-1: not known)
   std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through
+  std::vector<std::vector<uint32_t>> unit_idx;  // after a pattern round: the candidates' pattern indices
+  std::vector<uint32_t> unit_dmask;        // ... and the index bits D of their pairing (0: none)
   std::vector<Part> parts;
   std::vector<PatternUnit> punits;         // this round's pattern-tested units
   bgv_stats st{};
@@ -437,10 +493,6 @@ static int exec_reserve_groups(Exec& x, uint32_t groups) {
 }
 
 static int exec_create(Exec* x) {
-  HIPCHK(hipStreamCreateWithFlags(&x->main, hipStreamNonBlocking));
-  int least = 0, greatest = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  HIPCHK(hipStreamCreateWithPriority(&x->close, hipStreamNonBlocking, greatest));
   HIPCHK(hipEventCreate(&x->ev0));
   HIPCHK(hipEventCreate(&x->ev1));
   HIPCHK(hipEventCreateWithFlags(&x->ev_sets, hipEventDisableTiming));
@@ -469,8 +521,6 @@ static void exec_destroy(Exec* x) {
   for (auto& e : x->kev)
     if (e) (void)hipEventDestroy(e);
   if (x->close) (void)hipStreamSynchronize(x->close);
-  if (x->main) (void)hipStreamDestroy(x->main);
-  if (x->close) (void)hipStreamDestroy(x->close);
   delete x;
 }
 
@@ -672,6 +722,8 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
         call->units.emplace_back();
         call->unit_group.push_back(first_bad_shared);
         call->unit_rounds.push_back(0);
+        call->unit_idx.emplace_back();
+        call->unit_dmask.push_back(0);
       }
       if (!seen[j]) {
         seen[j] = 1;
@@ -770,6 +822,38 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
       call->punits.push_back(std::move(pu));
       continue;
     }
+    if (in_group && urounds > 0 && call->unit_dmask[ui] && call->unit_idx[ui].size() == u.size()) {
+      // pairs x, x ^ D of a pattern round's candidates (see PatternUnit), single jobs otherwise
+      const bgv_dgroup& g = call->L.groups[ug];
+      const uint32_t D = call->unit_dmask[ui];
+      const uint32_t b0 = D & (~D + 1);  // lowest bit of D
+      std::unordered_map<uint32_t, size_t> at;
+      for (size_t k = 0; k < u.size(); ++k) at[call->unit_idx[ui][k]] = u[k];
+      PatternUnit pu;
+      pu.group = (uint32_t)ug;
+      pu.kind = 1;
+      for (size_t k = 0; k < u.size(); ++k) {
+        const uint32_t x = call->unit_idx[ui][k];
+        const auto partner = at.find(x ^ D);
+        if (partner != at.end() && (x & b0)) continue;  // tested with its partner
+        std::vector<size_t> tj{u[k]};
+        uint64_t m = job_mask(call, u[k], g);
+        if (partner != at.end()) {
+          tj.push_back(partner->second);
+          m |= job_mask(call, partner->second, g);
+        }
+        Part part;
+        part.jobs = tj;
+        part.groups.push_back((uint32_t)rg.size());
+        part.pattern = (int)call->punits.size();
+        pu.tests.push_back((uint32_t)rg.size());
+        pu.test_jobs.push_back(std::move(tj));
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, 0, 0});
+        call->parts.push_back(std::move(part));
+      }
+      call->punits.push_back(std::move(pu));
+      continue;
+    }
     if (in_group && (urounds > 0 || u.size() <= kSingletonMax)) {
       // one device group per job, each masked to the job's slots: every verdict in this round
       const bgv_dgroup& g = call->L.groups[ug];
@@ -808,6 +892,8 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
   call->units.clear();
   call->unit_group.clear();
   call->unit_rounds.clear();
+  call->unit_idx.clear();
+  call->unit_dmask.clear();
 }
 
 static bool trace_on() {
@@ -828,9 +914,39 @@ static void call_after_round(Call* call, const int32_t* rv) {
       call->units.push_back(part.jobs);
       call->unit_group.push_back(-1);
       call->unit_rounds.push_back(0);
+      call->unit_idx.emplace_back();
+      call->unit_dmask.push_back(0);
     }
   }
   for (const PatternUnit& pu : call->punits) {
+    if (pu.kind == 1) {  // pairs and single jobs (see PatternUnit)
+      std::vector<size_t> failing;
+      for (size_t t = 0; t < pu.tests.size(); ++t)
+        if (!(rv[pu.tests[t]] & 1)) failing.push_back(t);
+      std::vector<size_t> again;
+      for (size_t t = 0; t < pu.tests.size(); ++t) {
+        const auto& tj = pu.test_jobs[t];
+        const bool pass = rv[pu.tests[t]] & 1;
+        if (pass || tj.size() == 1 || failing.size() == 1) {
+          for (size_t j : tj) call->code[j] = pass ? 1 : 0;
+        } else {
+          again.insert(again.end(), tj.begin(), tj.end());
+        }
+      }
+      if (failing.empty()) again = [&] {  // never expected: every job alone
+        std::vector<size_t> all;
+        for (const auto& tj : pu.test_jobs) all.insert(all.end(), tj.begin(), tj.end());
+        return all;
+      }();
+      if (!again.empty()) {
+        call->units.push_back(again);
+        call->unit_group.push_back((int)pu.group);
+        call->unit_rounds.push_back(2);
+        call->unit_idx.emplace_back();
+        call->unit_dmask.push_back(0);
+      }
+      continue;
+    }
     const size_t n = pu.jobs.size(), k = pu.tests.size();
     std::vector<size_t> cand;
     for (size_t i = 0; i < n; ++i) {
@@ -845,10 +961,20 @@ static void call_after_round(Call* call, const int32_t* rv) {
     if (cand.size() == 1) {
       call->code[cand[0]] = 0;  // the group failed and every invalid job is a candidate
     } else {
-      // two or more invalid jobs (or, never expected, none left: test every job alone)
+      // two or more invalid jobs (or, never expected, none left: test every job alone); D =
+      // the bits where S_b and its complement both failed
+      uint32_t D = 0;
+      for (size_t b = 0; b < k; ++b)
+        if (!(rv[pu.tests[b]] & 1) && !((rv[pu.tests[b]] >> 1) & 1)) D |= 1u << b;
+      std::vector<uint32_t> idx;
+      if (!cand.empty())
+        for (size_t i = 0; i < n; ++i)
+          if (std::find(cand.begin(), cand.end(), pu.jobs[i]) != cand.end()) idx.push_back((uint32_t)i);
       call->units.push_back(cand.empty() ? pu.jobs : cand);
       call->unit_group.push_back((int)pu.group);
       call->unit_rounds.push_back(1);
+      call->unit_dmask.push_back(cand.empty() ? 0 : D);
+      call->unit_idx.push_back(std::move(idx));
     }
   }
   call->parts.clear();
@@ -860,9 +986,19 @@ static double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
-static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) {
+
+static bool needs_retry(const std::vector<Call*>& calls) {
+  for (const Call* call : calls)
+    if (!call->units.empty()) return true;
+  return false;
+}
+
+// The first pass of one merged super-batch on the dispatcher's stream x.main: layout merge,
+// per-set kernels, the groups' closing, verdicts; leaves the retry units in the calls.
+static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, BatchState& bs) {
   const auto tb = std::chrono::steady_clock::now();
-  double t_merge = 0, t_tok = 0, t_sets = 0, t_pass1 = 0, t_post = 0, t_retry = 0;
+  bs.tb = tb;
+  double t_merge = 0, t_tok = 0, t_sets = 0, t_pass1 = 0, t_post = 0;
   // merge the calls' layouts
   uint32_t nslots = 0, ngroups = 0;
   size_t nidx = 0, npkb = 0, nuniq = 0;
@@ -932,14 +1068,12 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   b.uniq = x.d_idx + nidx;
   b.nuniq = (uint32_t)nuniq;
   bgv_streams S{x.main, prof ? x.kev : nullptr};
-  bgv_streams SC{x.close, prof ? x.kev : nullptr};
   int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;
   {
     // One super-batch at a time runs k_prep (the token); the token passes on as
     // soon as k_prep is done, so the next batch's k_prep waves queue behind this
     // batch's k_miller and take each SIMD as a Miller wave retires (no drain
-    // bubble between batches).  The latency-bound group closing runs on the
-    // high-priority stream and overlaps both.
+    // bubble between batches).  The group closing follows on the same stream.
     const auto tt = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> tok(*d.compute_mu);
     t_tok = ms_since(tt);
@@ -952,20 +1086,19 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     t_sets = ms_since(tt) - t_tok;
   }
   const auto tg = std::chrono::steady_clock::now();
-  HIPCHK(hipStreamWaitEvent(x.close, x.ev_sets, 0));
-  HIPCHK(bgv_launch_groups(b, SC, false));
-  HIPCHK(hipEventRecord(x.ev1, x.close));
-  HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
-  HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.close));
-  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.close));
-  HIPCHK(hipStreamSynchronize(x.close));
+  HIPCHK(bgv_launch_groups(b, S, false));
+  HIPCHK(hipEventRecord(x.ev1, x.main));
+  HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
+  HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
+  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.main));
+  HIPCHK(hipStreamSynchronize(x.main));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
   if (prof) prof_add(c, x, true, true);
   t_pass1 = ms_since(tg);
   const auto tp = std::chrono::steady_clock::now();
-  std::vector<uint32_t> call_gb;  // each call's first group in the merged batch
-  bool want_gu = false;
+  std::vector<uint32_t>& call_gb = bs.call_gb;
+  bool& want_gu = bs.want_gu;
   {
     uint32_t gb = 0;
     for (Call* call : calls) {
@@ -978,7 +1111,7 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
   }
   if (want_gu) {  // the first pass's u values of the groups, before a retry round reuses the array
     if ((rc = grow(&x.d_gu1, &x.gu1_cap, ngroups))) return rc;
-    HIPCHK(hipMemcpyAsync(x.d_gu1, b.gu, sizeof(fp12_t) * ngroups, hipMemcpyDeviceToDevice, x.close));
+    HIPCHK(hipMemcpyAsync(x.d_gu1, b.gu, sizeof(fp12_t) * ngroups, hipMemcpyDeviceToDevice, x.main));
   }
   {
     // bgv_verify_partial calls: the product of the call's groups (before any retry round
@@ -998,19 +1131,47 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       for (Call* call : calls) {
         const uint32_t ng = (uint32_t)call->L.groups.size();
         if (call->partial_out) {
-          HIPCHK(bgv_launch_partial(b, gb, ng, x.d_pscratch, x.d_pout, x.close));
-          HIPCHK(hipMemcpyAsync(call->partial_out, x.d_pout, 576, hipMemcpyDeviceToHost, x.close));
-          HIPCHK(hipStreamSynchronize(x.close));
+          HIPCHK(bgv_launch_partial(b, gb, ng, x.d_pscratch, x.d_pout, x.main));
+          HIPCHK(hipMemcpyAsync(call->partial_out, x.d_pout, 576, hipMemcpyDeviceToHost, x.main));
+          HIPCHK(hipStreamSynchronize(x.main));
         }
         gb += ng;
       }
     }
   }
+  HIPCHK(hipStreamSynchronize(x.main));  // the u copy, before the Exec changes hands
   t_post = ms_since(tp);
+  bs.t_merge = t_merge;
+  bs.t_tok = t_tok;
+  bs.t_sets = t_sets;
+  bs.t_pass1 = t_pass1;
+  bs.t_post = t_post;
+  bs.nslots = nslots;
+  bs.ngroups = ngroups;
+  bs.prof = prof;
+  if (trace_on() && !needs_retry(calls))
+    fprintf(stderr,
+            "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
+            "total %.1f ms\n",
+            d.id, calls.size(), nslots, ngroups, t_merge, t_tok, t_sets, t_pass1, t_post, ms_since(tb));
+  return BGV_OK;
+}
+
+// The retry rounds of a super-batch after run_pass1, on x.close (the device's retry stream),
+// over the per-slot results the first pass left in x's buffers.
+static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, BatchState& bs) {
+  const uint32_t nslots = bs.nslots;
+  const std::vector<uint32_t>& call_gb = bs.call_gb;
+  const bool want_gu = bs.want_gu, prof = bs.prof;
+  bgv_streams SC{x.close, prof ? x.kev : nullptr};
+  bgv_dev_batch b;
+  float ms = 0;
+  int rc;
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
   // retry rounds over the per-slot results on the device
   for (;;) {
+    const auto th = std::chrono::steady_clock::now();
     std::vector<bgv_dgroup> rg;
     std::vector<uint32_t> base;
     for (size_t k = 0; k < calls.size(); ++k) {
@@ -1030,19 +1191,24 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
     bool pattern = false;
     for (Call* call : calls) pattern = pattern || !call->punits.empty();
     if (pattern) b.gu1 = x.d_gu1;
+    const double t_build = ms_since(th);
+    const auto tl = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(x.ev0, x.close));
     HIPCHK(bgv_launch_groups(b, SC, true));
     HIPCHK(hipEventRecord(x.ev1, x.close));
     HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
     HIPCHK(hipStreamSynchronize(x.close));
+    const double t_wait = ms_since(tl);
     HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
     if (prof) prof_add(c, x, false, true);
     if (trace_on()) {
       size_t npt = 0;
       for (Call* call : calls)
         for (const PatternUnit& pu : call->punits) npt += pu.tests.size();
-      fprintf(stderr, "[bgv]  round %d: %u groups (%zu pattern tests), device %.2f ms, since round start %.1f ms\n",
-              rounds, nrg, npt, ms, ms_since(tr));
+      fprintf(stderr,
+              "[bgv]  round %d: %u groups (%zu tests with a reference), host %.2f, launch..verdicts %.2f, device %.2f ms, "
+              "since round start %.1f ms\n",
+              rounds, nrg, npt, t_build, t_wait, ms, ms_since(tr));
     }
     for (size_t k = 0; k < calls.size(); ++k) {
       Call* call = calls[k];
@@ -1054,16 +1220,66 @@ static int run_batch(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls) 
       call_after_round(call, rv);
     }
   }
-  t_retry = ms_since(tr);
+  const double t_retry = ms_since(tr);
   if (trace_on())
     fprintf(stderr,
             "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
             "retry(%d) %.1f total %.1f ms\n",
-            d.id, calls.size(), nslots, ngroups, t_merge, t_tok, t_sets, t_pass1, t_post, rounds, t_retry, ms_since(tb));
+            d.id, calls.size(), nslots, bs.ngroups, bs.t_merge, bs.t_tok, bs.t_sets, bs.t_pass1, bs.t_post, rounds,
+            t_retry, ms_since(bs.tb));
   return BGV_OK;
 }
 
-static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
+static Exec* exec_acquire(Device& d) {
+  DevSched& s = *d.sched;
+  std::unique_lock<std::mutex> lk(s.mu);
+  s.cv.wait(lk, [&s] { return !s.free.empty(); });
+  Exec* x = s.free.front();
+  s.free.pop_front();
+  return x;
+}
+
+static void exec_release(Device& d, Exec* x) {
+  DevSched& s = *d.sched;
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    s.free.push_back(x);
+  }
+  s.cv.notify_all();
+}
+
+static void finish_calls(std::vector<Call*>& calls, int rc) {
+  for (Call* call : calls) {
+    if (rc != BGV_OK)
+      call_fail(call, rc);
+    else
+      call_finish(call);
+  }
+}
+
+// The device's retry thread: the retry rounds of handed-over super-batches, in order; drains
+// the queue before it stops.
+static void retry_loop(bgv_ctx* c, Device* d) {
+  DevSched& s = *d->sched;
+  (void)hipSetDevice(d->id);
+  for (;;) {
+    RetryJob job;
+    {
+      std::unique_lock<std::mutex> lk(s.mu);
+      s.cv.wait(lk, [&s] { return s.stop || !s.rq.empty(); });
+      if (s.rq.empty()) return;
+      job = std::move(s.rq.front());
+      s.rq.pop_front();
+    }
+    job.x->close = s.retry;
+    const int rc = run_retries(c, *d, *job.x, job.calls, *job.st);
+    finish_calls(job.calls, rc);
+    exec_release(*d, job.x);
+  }
+}
+
+static void dispatcher_loop(bgv_ctx* c, Device* d, hipStream_t stream) {
+  (void)hipSetDevice(d->id);
   for (;;) {
     std::vector<Call*> calls;
     {
@@ -1098,19 +1314,27 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, Exec* x) {
       }
       if (!c->queue.empty()) c->qcv.notify_one();
     }
+    Exec* x = exec_acquire(*d);
+    x->main = stream;
+    auto bs = std::make_shared<BatchState>();
     int rc;
     {
       std::shared_lock<std::shared_mutex> clk(c->cache_mu);
       c->running.fetch_add(1);
-      rc = run_batch(c, *d, *x, calls);
+      rc = run_pass1(c, *d, *x, calls, *bs);
       c->running.fetch_sub(1);
     }
-    for (Call* call : calls) {
-      if (rc != BGV_OK)
-        call_fail(call, rc);
-      else
-        call_finish(call);
+    if (rc == BGV_OK && needs_retry(calls)) {
+      DevSched& s = *d->sched;
+      {
+        std::lock_guard<std::mutex> lk(s.mu);
+        s.rq.push_back(RetryJob{std::move(calls), x, bs});
+      }
+      s.cv.notify_all();
+      continue;
     }
+    finish_calls(calls, rc);
+    exec_release(*d, x);
   }
 }
 
@@ -1125,6 +1349,11 @@ static void ctx_free_devices(bgv_ctx* c) {
     (void)hipSetDevice(d.id);
     for (Exec* x : d.execs) exec_destroy(x);
     d.execs.clear();
+    d.sched->free.clear();
+    for (hipStream_t st : d.sched->dstreams) (void)hipStreamDestroy(st);
+    d.sched->dstreams.clear();
+    if (d.sched->retry) (void)hipStreamDestroy(d.sched->retry);
+    d.sched->retry = nullptr;
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
@@ -1160,10 +1389,19 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     d.id = (devices && ndev > 0) ? devices[i] : 0;
     bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
               hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
+    int least = 0, greatest = 0;
+    ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+         hipStreamCreateWithPriority(&d.sched->retry, hipStreamNonBlocking, greatest) == hipSuccess;
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
+      hipStream_t st = nullptr;
+      ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+      if (ok) d.sched->dstreams.push_back(st);
+    }
+    for (int k = 0; ok && k < execs_per_device(); ++k) {
       Exec* x = new Exec();
       d.execs.push_back(x);
       ok = exec_create(x) == BGV_OK;
+      if (ok) d.sched->free.push_back(x);
     }
     if (!ok) {
       ctx_free_devices(c);
@@ -1172,8 +1410,10 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
       return d.id < 0 || d.id >= avail ? -BGV_E_ARG : -BGV_E_DEVICE;
     }
   }
-  for (Device& d : c->devs)
-    for (Exec* x : d.execs) c->dispatchers.emplace_back(dispatcher_loop, c, &d, x);
+  for (Device& d : c->devs) {
+    for (hipStream_t st : d.sched->dstreams) c->dispatchers.emplace_back(dispatcher_loop, c, &d, st);
+    d.sched->retry_thread = std::thread(retry_loop, c, &d);
+  }
   *out = c;
   return BGV_OK;
 }
@@ -1188,6 +1428,15 @@ int bgv_close(bgv_ctx* c) {
   for (auto& w : c->dispatchers)
     if (w.joinable()) w.join();
   c->dispatchers.clear();
+  // the retry threads finish the super-batches handed to them, then stop
+  for (Device& d : c->devs) {
+    {
+      std::lock_guard<std::mutex> lk(d.sched->mu);
+      d.sched->stop = true;
+    }
+    d.sched->cv.notify_all();
+    if (d.sched->retry_thread.joinable()) d.sched->retry_thread.join();
+  }
   std::unique_lock<std::shared_mutex> lk(c->cache_mu);
   if (c->closed.exchange(true)) return BGV_OK;
   ctx_free_devices(c);

@@ -82,7 +82,11 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   const bool live = team < BGV_FINAL12_TEAMS && gi < ngroups;
   // teams past the end (and the idle sixth) read the last group and multiply by 1
   const bgv_dgroup g = groups[live ? gi : ngroups - 1];
-  if (c == 0) lens[team] = live ? g.n_slots : 0;
+  // the group's slots (<= 64, bgv_launch_groups) as a bit set: the product runs over the
+  // present ones only (a retry test masks half of a group or a single job), the teams of the
+  // wave to the longest list, multiplying by 1 past their own
+  uint64_t m = live ? g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1)) : 0;
+  if (c == 0) lens[team] = (uint32_t)__popcll(m);
   __syncthreads();
   uint32_t nmax = 0;
   BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
@@ -92,9 +96,15 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
   constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
   fp_t x = reinterpret_cast<const fp_t*>(gpair + (live ? gi : ngroups - 1))[fi];
-  fp_t y = live && grp_has(g, 0) ? fs[fi] : one_c;
+  auto next = [&]() {  // the next present slot's coefficient, or 1
+    if (!m) return one_c;
+    const int k = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    return fs[kFp12 * k + fi];
+  };
+  fp_t y = next();
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-    const fp_t yn = live && grp_has(g, k + 1) ? fs[kFp12 * (k + 1) + fi] : one_c;
+    const fp_t yn = next();  // next operand in flight
     x = o.mul(x, y);
     y = yn;
   }

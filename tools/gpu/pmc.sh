@@ -3,7 +3,7 @@
 # isolated roofline call.  Outputs under gpurun_out/s3/<TAG>_pmc.
 set -o pipefail
 TAG=${TAG:-roof}
-D=gpurun_out/${TAG}_pmc
+D=gpurun_out/${TAG}/pmc
 mkdir -p $D
 export TMPDIR=/tmp
 i=0
