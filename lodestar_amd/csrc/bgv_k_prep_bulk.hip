@@ -21,11 +21,12 @@ __global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint3
                                       const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                       const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
                                       int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg,
-                                      const uint32_t* __restrict__ uniq, uint32_t nuniq) {
+                                      const uint32_t* __restrict__ uniq, uint32_t nuniq, uint32_t task0) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t task = blockIdx.y + task0;
   // hash first: the longest task starts earliest.  With uniq, lane u hashes the u-th distinct
   // signing root (slot uniq[u]); lanes past nuniq -- whole waves of them -- exit at once.
-  if (blockIdx.y == 0) {
+  if (task == 0) {
     if (uniq) {
       if (s < nuniq) task_hash(uniq[s], slots, h);
     } else if (s < nslots) {
@@ -34,7 +35,7 @@ __global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint3
     return;
   }
   if (s >= nslots) return;
-  if (blockIdx.y == 1)
+  if (task == 1)
     task_sig(s, slots, rsig, sig_status);
   else
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
@@ -42,9 +43,16 @@ __global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint3
 
 }  // extern "C"
 
+// BGV_PREP_SPLIT=1 (profiling only: per-task kernel time and counters): the three tasks as
+// three launches of k_prep, one plane each, in the same order
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree) {
-  hipLaunchKernelGGL(k_prep, dim3(nblk(b.nslots, 64), 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig, b.sig_status,
-                     b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                     tree ? b.pk_agg : nullptr, b.uniq, b.nuniq);
+  static const bool split = [] {
+    const char* e = getenv("BGV_PREP_SPLIT");
+    return e && atoi(e) > 0;
+  }();
+  for (uint32_t t0 = 0; t0 < 3; t0 += split ? 1 : 3)
+    hipLaunchKernelGGL(k_prep, dim3(nblk(b.nslots, 64), split ? 1 : 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig,
+                       b.sig_status, b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk,
+                       b.pk_status, tree ? b.pk_agg : nullptr, b.uniq, b.nuniq, t0);
   return hipGetLastError();
 }
