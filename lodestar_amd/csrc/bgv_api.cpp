@@ -197,8 +197,8 @@ struct RetryJob {
 // retry thread and goes on with the next super-batch; the Exec returns to the pool when the
 // retry rounds are done.  So the latency-bound retry rounds of one batch overlap the per-set
 // kernels of the next ones instead of holding a dispatcher.  Streams: one per dispatcher, one
-// (high priority) for the retry rounds, the utility stream: within the device's 4 hardware
-// queues (GPU_MAX_HW_QUEUES).
+// (high priority) for the retry rounds, the utility stream: within HIP's default of 4 hardware
+// queues per process (GPU_MAX_HW_QUEUES).
 struct DevSched {
   std::mutex mu;
   std::condition_variable cv;  // an Exec was released / a retry job was queued / stop
