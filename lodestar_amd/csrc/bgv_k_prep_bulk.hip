@@ -45,22 +45,12 @@ __global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint3
 
 // BGV_PREP_SPLIT=1 (profiling only: per-task kernel time and counters): the three tasks as
 // three launches of k_prep, one plane each, in the same order
-// BGV_PREP_W2=mask: task t (bit t; 1 sig, 2 pk) as its own launch at two waves per SIMD (A/B)
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree) {
-  static const int w2 = [] {
-    const char* e = getenv("BGV_PREP_W2");
-    return e ? atoi(e) : 0;
-  }();
   static const bool split = [] {
     const char* e = getenv("BGV_PREP_SPLIT");
-    return (e && atoi(e) > 0) || w2;
+    return e && atoi(e) > 0;
   }();
   for (uint32_t t0 = 0; t0 < 3; t0 += split ? 1 : 3) {
-    if (split && ((w2 >> t0) & 1)) {
-      const hipError_t e = bgv_launch_prep_w2(b, s, tree, (int)t0);
-      if (e != hipSuccess) return e;
-      continue;
-    }
     hipLaunchKernelGGL(k_prep, dim3(nblk(b.nslots, 64), split ? 1 : 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig,
                        b.sig_status, b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk,
                        b.pk_status, tree ? b.pk_agg : nullptr, b.uniq, b.nuniq, t0);

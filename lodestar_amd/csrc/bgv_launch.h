@@ -76,8 +76,6 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // pr
 bool bgv_sig_pairs(const bgv_dev_batch& b);
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree);  // bgv_k_prep_bulk.hip
-// task 1 (sig) or 2 (pk) of the bulk k_prep at two waves per SIMD (bgv_k_prep_w2.hip)
-hipError_t bgv_launch_prep_w2(const bgv_dev_batch& b, const bgv_streams& s, bool tree, int task);
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
