@@ -1,9 +1,10 @@
 """GPU parity of the latency path (VERDICT r02 "missing #5").
 
-Calls of up to 16,384 pairs (all gossip and block import) run k_prep_a + k_prep_team
-(hash_to_G2 with generated team programs for the cofactor clearing, subgroup check and
-r * sig) and k_miller_team (one Miller loop per team of 16 lanes), a different
-implementation from the bulk path's task_hash / k_miller.  bgv_debug_prepare runs either
+Calls of up to 16,384 pairs (all gossip and block import) run k_prep_a and the generated
+point programs for the cofactor clearing, subgroup check and r * sig, then the table-driven
+Miller loop: up to 340 sets on whole blocks (k_prep_wide, k_miller_wide: four-part round
+instructions, wide Fp12 products), above on four sets per block (k_prep_team,
+k_miller_team) -- implementations different from the bulk path's task_hash / k_miller.  bgv_debug_prepare runs either
 path with the same randomizers and returns every set's H(m) and Miller-loop value f:
   * H(m) from both paths is byte-compared with the hash_to_G2 goldens (RFC 9380 suite,
     tests/golden/hash_to_g2.json from the oracle pinned by tests/test_oracle_kat.py);
@@ -91,3 +92,20 @@ def test_latency_vs_bulk_miller_values(ctx):
     # the randomizer enters f: another seed gives other values
     other = ctx.debug_prepare(sets[:4], native.PATH_BULK, seed=2)
     assert all(o[1] != b[1] for o, b in zip(other, ctx.debug_prepare(sets[:4], native.PATH_BULK, seed=3)))
+
+
+def test_latency_team_kernels_vs_bulk(ctx):
+    """Above BGV_PREP_WIDE_MAX (340) sets the latency path runs the four-sets-per-block team
+    point programs (k_prep_team), above BGV_MILLER_WIDE_MAX (1024) pairs the four-pairs-per-block
+    Miller loop (k_miller_team): same H(m), f and statuses as the bulk path."""
+    from lodestar_amd import native
+    base = _mixed_sets(ctx)
+    sets = []
+    while len(sets) < 1100:
+        sets += base
+    sets = sets[:1100]
+    bulk = ctx.debug_prepare(sets, native.PATH_BULK, seed=11)
+    lat = ctx.debug_prepare(sets, native.PATH_LATENCY, seed=11)
+    assert len(bulk) == len(lat) == 1100
+    for i, (b, l) in enumerate(zip(bulk, lat)):
+        assert b == l, i
