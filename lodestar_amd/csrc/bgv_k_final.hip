@@ -115,19 +115,20 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   if (live && c == 0) verdict[gi] = v;
 }
 
-// The latency path's closing (small calls): one block of 4 teams per group.  Team t
-// multiplies the group's slots t, t + 4, ... (team 0 also the signature pair), the four
-// partial products meet in LDS and every team forms the same product in the same order (a
-// quarter of k_final's serial product chain).  The final exponentiation then runs on the
+// The latency path's closing (small calls): one 128-thread block of 8 teams per group.  Team t
+// multiplies the group's slots t, t + 8, ... (team 0 also the signature pair), the eight
+// partial products meet in LDS in a three-level tree (an eighth of k_final's serial product
+// chain).  The final exponentiation then runs on the
 // whole block with each coefficient's products split over four lanes (tm_wide_ops): 2 + 1
 // double-width products per lane and squaring instead of 7 + 1.
-__global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+#define BGV_FOLD_TEAMS 8  // 16-lane teams of k_final_fold's 128-thread block
+__global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                        const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                        int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
                                        fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
                                        const fp12_t* __restrict__ fsig) {
-  __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
-  __shared__ fp_t part[BGV_FINAL_TEAMS][BGV_TEAM_COMPS];
+  __shared__ fp_t lds[BGV_FOLD_TEAMS][2 * BGV_TEAM_COMPS];
+  __shared__ fp_t part[BGV_FOLD_TEAMS][BGV_TEAM_COMPS];
   __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[4 * BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
@@ -141,18 +142,22 @@ __global__ void BGV_KATTR k_final_fold(const bgv_dgroup* __restrict__ groups, ui
   // the group's signature pair, or (fsig: bgv_sig_pairs) each slot's own
   fp_t x = team == 0 && !fsig ? reinterpret_cast<const fp_t*>(gpair + (gi < ngroups ? gi : ngroups - 1))[fi] : one_c;
   const fp_t* ss = fsig ? reinterpret_cast<const fp_t*>(fsig + g.first_slot) : nullptr;
-  const uint32_t nmax = (g.n_slots + BGV_FINAL_TEAMS - 1) / BGV_FINAL_TEAMS;
+  const uint32_t nmax = (g.n_slots + BGV_FOLD_TEAMS - 1) / BGV_FOLD_TEAMS;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-    const uint32_t idx = team + BGV_FINAL_TEAMS * k;
+    const uint32_t idx = team + BGV_FOLD_TEAMS * k;
     const bool in = grp_has(g, idx);
     const fp_t y = in ? fs[kFp12 * idx + fi] : one_c;
     x = o.mul(x, y);
     if (ss) x = o.mul(x, in ? ss[kFp12 * idx + fi] : one_c);  // grid-uniform branch
   }
-  if (c < BGV_TEAM_COMPS) part[team][cc] = x;
-  __syncthreads();
-  x = part[0][cc];
-  BGV_UNROLL for (int t = 1; t < BGV_FINAL_TEAMS; ++t) x = o.mul(x, part[t][cc]);
+  // the eight partial products as a tree: every team multiplies at every level (the barriers
+  // inside o.mul), team t keeps parts 2t and 2t + 1 of the level
+  BGV_UNROLL for (int w = BGV_FOLD_TEAMS; w > 1; w >>= 1) {
+    if (c < BGV_TEAM_COMPS) part[team][cc] = x;
+    __syncthreads();
+    const int t2 = 2 * (team % (w >> 1));
+    x = o.mul(part[t2][cc], part[t2 + 1][cc]);
+  }
   if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   // the final exponentiation on the whole block with the wide products (bgv_team_dev.h)
   if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
@@ -234,7 +239,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     if (e != hipSuccess) return e;
   }
   if (b.nslots + b.ngroups <= bgv_latency_max())
-    hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(64), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
+    hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(128), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,
                        !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
   else
