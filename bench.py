@@ -155,7 +155,7 @@ def default_batching():
         except ValueError:
             v = dflt
         return v if v >= 0 else dflt
-    return env("BGV_MAX_BATCH_SLOTS", 131072), env("BGV_COALESCE_US", 2000), env("BGV_IDLE_COALESCE_US", 200)
+    return env("BGV_MAX_BATCH_SLOTS", 131072), env("BGV_COALESCE_US", 500), env("BGV_IDLE_COALESCE_US", 50)
 
 
 def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0x8192, committee=1):

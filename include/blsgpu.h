@@ -216,7 +216,7 @@ int bgv_sign(bgv_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, size_t n, ui
  * multithread/index.ts:39-57,386-401).  While no super-batch is running the window is
  * idle_coalesce_us instead (at most coalesce_us), so a lone call launches at once.
  * max_batch_slots = 0 and a window of UINT32_MAX leave a value unchanged.  Defaults:
- * 131072 sets, 2000 us, 200 us (env BGV_MAX_BATCH_SLOTS, BGV_COALESCE_US,
+ * 131072 sets, 500 us, 50 us (env BGV_MAX_BATCH_SLOTS, BGV_COALESCE_US,
  * BGV_IDLE_COALESCE_US). */
 int bgv_set_batching(bgv_ctx* ctx, uint32_t max_batch_slots, uint32_t coalesce_us, uint32_t idle_coalesce_us);
 

@@ -76,7 +76,7 @@ static uint32_t group_slots() {
   return v;
 }
 // how long an idle dispatcher waits for more calls to merge (BGV_COALESCE_US env)
-#define BGV_COALESCE_US 2000
+#define BGV_COALESCE_US 500
 static size_t coalesce_us() {
   static const size_t v = env_size("BGV_COALESCE_US", BGV_COALESCE_US, 0);
   return v;
@@ -84,7 +84,7 @@ static size_t coalesce_us() {
 // the window while no super-batch is running: a lone call (block import, a quiet gossip
 // moment) then launches almost at once instead of waiting the full window for company
 // that is not coming (BGV_IDLE_COALESCE_US env)
-#define BGV_IDLE_COALESCE_US 200
+#define BGV_IDLE_COALESCE_US 50
 static size_t idle_coalesce_us() {
   static const size_t v = env_size("BGV_IDLE_COALESCE_US", BGV_IDLE_COALESCE_US, 0);
   return v;
