@@ -24,11 +24,13 @@ const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:39
 // Batchable buffering (index.ts:48,57 use 32 sets / 100 ms for CPU workers).  Gossip caps
 // concurrency per topic (64 for attestations, network/gossip/validation/queue.ts:14), so the
 // Node-level rate is concurrency / per-call latency: a long buffer wait only adds latency,
-// and the library already merges the calls in flight into super-batches.  Measured with 64
+// and the library already merges the calls in flight into super-batches.  The flush test is
+// the reference's `sigCount > maxBufferedSigs`, so 63 sends the buffer the moment a full
+// queue's 64 sets are in it; at 64 every batch waited for the timer.  Measured with 64
 // concurrent one-set callers on one MI355X (tests/node/gossip_bench.js,
-// profiles/r02/gossip_node_64callers_t6.jsonl): 32 sets / 100 ms 1.35k sets/s, 32 / 2 ms
-// 5.2k, 64 / 1 ms 5.7k sets/s at p50 11 ms.
-const MAX_BUFFERED_SIGS = 64;
+// profiles/r03/gossip/flush_at_callers.jsonl): 63 / 1 ms 11.6k sets/s at p50 5.4 ms,
+// 64 / 1 ms 9.9k at 6.4 ms, 32 / 100 ms 6.2k at 10.3 ms.
+const MAX_BUFFERED_SIGS = 63;
 const MAX_BUFFER_WAIT_MS = 1;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
@@ -190,7 +192,7 @@ class BlsGpuVerifier {
         }
       } else {
         this.jobs.push(job);
-        setTimeout(this.runJob, 0);
+        setImmediate(this.runJob);
       }
     });
   }
@@ -199,10 +201,13 @@ class BlsGpuVerifier {
     if (this.bufferedJobs) {
       this.jobs.push(...this.bufferedJobs.jobs);
       this.bufferedJobs = null;
-      setTimeout(this.runJob, 0);
+      setImmediate(this.runJob);
     }
   };
 
+  // Scheduled with setImmediate where index.ts uses setTimeout(runJob, 0): jobs queued in the
+  // same macrotask still leave in one call, without Node's 1 ms floor on a zero timeout (a
+  // whole millisecond on every gossip batch's critical path).
   // All queued jobs go to the device in one call; the library merges concurrent calls into
   // super-batches, so there is no idle-worker bookkeeping here (index.ts:290-381).
   runJob = async () => {

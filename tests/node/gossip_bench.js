@@ -5,14 +5,14 @@
 // (verifySignatureSets([set], {batchable: true}), as validateGossipAttestation does), for
 // `seconds`, over one verifier.  Prints one JSON line per buffering setting with sets/s and
 // per-call latency percentiles.
-//   node gossip_bench.js [seconds=8] [callers=64] [settings="32:100,1024:20,64:5,32:2"]
+//   node gossip_bench.js [seconds=8] [callers=64] [settings="63:1,64:1,32:100,16:1"]
 const path = require("path");
 const crypto = require("crypto");
 const {BlsGpuVerifier, addon} = require(path.join(__dirname, "..", "..", "lodestar_amd", "node", "BlsGpuVerifier.js"));
 
 const seconds = Number(process.argv[2] || 8);
 const callers = Number(process.argv[3] || 64);
-const settings = (process.argv[4] || "32:100,1024:20,64:5,32:2").split(",").map((s) => s.split(":").map(Number));
+const settings = (process.argv[4] || "63:1,64:1,32:100,16:1").split(",").map((s) => s.split(":").map(Number));
 const NKEYS = 16384;
 
 function pct(xs, p) {
