@@ -1,4 +1,9 @@
+# lin combinations with i32 x i32 multiply-adds: config-3 latency kernels, latency-path GPU parity
 set -o pipefail
 O=gpurun_out/r03v; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_r03.py -m gpu -v --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1 || { echo failed; tail -30 $O/pytest.txt; exit 1; }
-tail -5 $O/pytest.txt
+timeout -k 10 120 python tools/gpu/latency_probe.py 40 > $O/lat.json 2>>$O/err || exit 1
+cat $O/lat.json
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python tools/gpu/latency_probe.py 20 > $O/prof.txt 2>&1 || exit 1
+cut -d, -f1-4 $O/prof/run_kernel_stats.csv | head -8
+timeout -k 10 700 python -u -m pytest -x -q -m gpu --timeout 120 --timeout-method thread tests > $O/pytest.txt 2>&1; echo pytest rc=$?; tail -2 $O/pytest.txt
