@@ -8,12 +8,14 @@
 //   no_redc   the product kept (generic tmp_lin), the REDC replaced by a fold of the wide accumulator
 //   lin_only  the two operand combinations (templated) summed, no product
 //   prod_only product + REDC of two slots read directly (no combinations)
+//   engine    the production engine (bgv_tround_dev.h tr_wide_engine)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I lodestar_amd/csrc tools/ubench_round.hip -o /tmp/ubench_round
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
 #include "bgv_tcurve.h"
 #include "bls_team.h"
+#include "bgv_tround_dev.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 1; } } while (0)
@@ -74,6 +76,10 @@ struct ub_engine {
   __device__ void check_add() {}
 };
 
+struct ub_prod_engine : tr_wide_engine {
+  __device__ void check_add() {}
+};
+
 template <int V>
 __global__ void __launch_bounds__(64) k_round(uint32_t* out, int reps) {
   __shared__ uint8_t prog[TCP_TABLE_BYTES];
@@ -87,9 +93,14 @@ __global__ void __launch_bounds__(64) k_round(uint32_t* out, int reps) {
     S[i] = x;
   }
   __syncthreads();
-  ub_engine<V> e{prog, S, RP, lane % BGV_TEAM, lane / BGV_TEAM};
   int a = 0;
-  for (int k = 0; k < reps; ++k) a += tc_mul_x_abs(e);
+  if (V == 6) {
+    ub_prod_engine e{{prog, S, RP, lane % BGV_TEAM, lane / BGV_TEAM, false}};
+    for (int k = 0; k < reps; ++k) a += tc_mul_x_abs(e);
+  } else {
+    ub_engine<V> e{prog, S, RP, lane % BGV_TEAM, lane / BGV_TEAM};
+    for (int k = 0; k < reps; ++k) a += tc_mul_x_abs(e);
+  }
   if (lane == 0) out[blockIdx.x] = S[a % TCP_NSLOT].v[0];
 }
 
@@ -122,7 +133,7 @@ int main() {
   CHECK(hipMalloc(&d, sizeof(uint32_t) * 1024));
   for (int blocks : {131})
     if (run<0>("real", d, blocks) || run<1>("no_sum", d, blocks) || run<2>("no_prod", d, blocks) ||
-        run<3>("no_redc", d, blocks) || run<4>("lin_only", d, blocks) || run<5>("prod_only", d, blocks))
+        run<3>("no_redc", d, blocks) || run<4>("lin_only", d, blocks) || run<5>("prod_only", d, blocks) || run<6>("engine", d, blocks))
       return 1;
   CHECK(hipFree(d));
   return 0;
