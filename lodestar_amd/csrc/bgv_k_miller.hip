@@ -163,26 +163,30 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
   }
 }
 
-// The same pairs with one pair per 64-lane block for the smallest calls: the twist-point
-// rounds of k_miller_team as four-part instructions on all 64 lanes (bgv_tround_dev.h), and
-// the Fp12 accumulator with the wide products (bgv_team_dev.h tm_wide_ops: each coefficient's
-// double-width products split over four lanes), so a doubling step waits 6 + 3 + 3 product
-// latencies instead of 10 + 8 + 7.  Same formulas, same field element as k_miller_team.
-// rsig non-null (bgv_sig_pairs): blocks [nslots, 2 nslots) pair the slots' own r_i sig_i with
-// -G1 into fsig instead of pairing group sums.
-__global__ void __launch_bounds__(64) k_miller_wide(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                                    const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
-                                                    const int32_t* __restrict__ sig_status,
-                                                    const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
-                                                    uint32_t ngroups, const g2_jac* __restrict__ gsum,
-                                                    fp12_t* __restrict__ gpair, const g2_jac* __restrict__ rsig,
-                                                    fp12_t* __restrict__ fsig) {
+// The same pairs with one pair per block for the smallest calls, on two waves that run the
+// loop's two chains side by side: wave 0 the twist-point rounds of k_miller_team as
+// four-part instructions (bgv_tround_dev.h), wave 1 the Fp12 accumulator with the wide
+// products (bgv_team_dev.h tm_wide_ops: each coefficient's double-width products split over
+// four lanes).  The point rounds of step i need nothing from the accumulator, so wave 0
+// computes step i's lines while wave 1 applies step i + 1's (square, line products); the
+// lines pass through a two-entry LDS ring with one block barrier per step, and a step costs
+// the longer of the two chains instead of their sum.  Same formulas, same field element as
+// k_miller_team.  rsig non-null (bgv_sig_pairs): blocks [nslots, 2 nslots) pair the slots'
+// own r_i sig_i with -G1 into fsig instead of pairing group sums.
+__global__ void __launch_bounds__(128) k_miller_wide(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                                     const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
+                                                     const int32_t* __restrict__ sig_status,
+                                                     const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
+                                                     uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                                     fp12_t* __restrict__ gpair, const g2_jac* __restrict__ rsig,
+                                                     fp12_t* __restrict__ fsig) {
   __shared__ uint8_t prog[TMP_TABLE_BYTES];
   __shared__ fp_t Sm[TMP_NSLOT];
   __shared__ fp_t WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[4 * BGV_TEAM_COMPS], RP[64];
-  for (int i = threadIdx.x; i < TMP_TABLE_BYTES; i += 64) prog[i] = kTmProg[i];
-  const int lane = threadIdx.x, c = lane % BGV_TEAM;  // c: lane of the twist-point rounds (< 16)
-  const uint32_t uu = blockIdx.x;                     // grid = exactly nslots + ngroups blocks
+  __shared__ fp_t LR[2][2][6];  // [step & 1][addition line, doubling line][l0, l1, l3 as Fp pairs]
+  for (int i = threadIdx.x; i < TMP_TABLE_BYTES; i += 128) prog[i] = kTmProg[i];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t uu = blockIdx.x;  // grid = exactly nslots + ngroups blocks
   const bool set_pair = uu < nslots;
   bool live;
   const fp_t* qsrc;
@@ -197,48 +201,78 @@ __global__ void __launch_bounds__(64) k_miller_wide(const bgv_dslot* __restrict_
     qsrc = reinterpret_cast<const fp_t*>(gsum + j);
     live = !jac_is_inf(gsum[j]);
   }
-  if (lane < 6) {
-    const fp_t v = live ? qsrc[lane] : fp_zero();
-    Sm[TMP_S_QX + lane] = v;
-    Sm[TMP_S_BANK0 + lane] = v;
-  } else if (lane < 9) {
-    const g1_jac P = set_pair ? rpk[uu] : jac_from_aff(g1_neg_generator());
-    const fp_t v = lane == 6 ? fp_neg(fp_mul(P.x, P.z)) : (lane == 7 ? P.y : fp_mul(fp_sqr(P.z), P.z));
-    Sm[lane == 6 ? TMP_S_XN : (lane == 7 ? TMP_S_YP : TMP_S_ZP3)] = live ? v : fp_zero();
-  } else if (lane == 9) {
-    Sm[TMP_S_ONE] = fp_one();
+  if (w == 0) {
+    if (lane < 6) {
+      const fp_t v = live ? qsrc[lane] : fp_zero();
+      Sm[TMP_S_QX + lane] = v;
+      Sm[TMP_S_BANK0 + lane] = v;
+    } else if (lane < 9) {
+      const g1_jac P = set_pair ? rpk[uu] : jac_from_aff(g1_neg_generator());
+      const fp_t v = lane == 6 ? fp_neg(fp_mul(P.x, P.z)) : (lane == 7 ? P.y : fp_mul(fp_sqr(P.z), P.z));
+      Sm[lane == 6 ? TMP_S_XN : (lane == 7 ? TMP_S_YP : TMP_S_ZP3)] = live ? v : fp_zero();
+    } else if (lane == 9) {
+      Sm[TMP_S_ONE] = fp_one();
+    }
   }
   __syncthreads();
-  tr_wide_engine eng{prog, Sm, RP, c, lane / BGV_TEAM, false};
-  auto run = [&](int off) { eng.run(off); };
-  tm_wide_ops o{WA, WB, WP, lane % BGV_TEAM_COMPS, lane / BGV_TEAM_COMPS};
-  run(TMP_INIT);
-  run(TMP_DBL0);
+  tr_wide_engine eng{prog, Sm, RP, lane % BGV_TEAM, lane / BGV_TEAM, false};
+  // wave 0: the line of the last program run into ring entry (r, k)
+  auto post = [&](int r, int k) {
+    if (lane < 6) LR[r][k][lane] = Sm[(lane < 2 ? TMP_S_L0 : (lane < 4 ? TMP_S_L1 - 2 : TMP_S_L3 - 4)) + lane];
+  };
+  tm_wide_ops_t<true> o{WA, WB, WP, lane % BGV_TEAM_COMPS, lane / BGV_TEAM_COMPS};
+  auto ln = [&](int r, int k, fp2_t* l0, fp2_t* l1, fp2_t* l3) {
+    const fp_t* L = LR[r][k];
+    *l0 = fp2_t{L[0], L[1]};
+    *l1 = fp2_t{L[2], L[3]};
+    *l3 = fp2_t{L[4], L[5]};
+  };
+  fp_t x;
+  if (w == 0) {
+    eng.run(TMP_INIT);
+    eng.run(TMP_DBL0);
+    post(0, 1);
+  }
+  __syncthreads();
+  if (w == 1) {
+    fp2_t l0, l1, l3;
+    ln(0, 1, &l0, &l1, &l3);
+    x = o.line(l0, l1, l3);
+  }
+  // step i (61..0): wave 0 computes its lines into ring entry i & 1 while wave 1 applies step
+  // i + 1's from entry (i + 1) & 1; the barrier ends both
   int bank = 1;
-  fp2_t l0 = {Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]}, l1 = {Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]},
-        l3 = {Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
-  fp_t x = o.line(l0, l1, l3);
-  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
-    if (tmp_add_at(i)) {
-      run(bank ? TMP_ADD1 : TMP_ADD0);
-      bank ^= 1;
-      l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
-      l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
-      l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
+  BGV_NO_UNROLL for (int i = 61; i >= -1; --i) {
+    if (w == 0) {
+      if (i >= 0) {
+        if (tmp_add_at(i)) {
+          eng.run(bank ? TMP_ADD1 : TMP_ADD0);
+          bank ^= 1;
+          post(i & 1, 0);
+        }
+        eng.run(bank ? TMP_DBL1 : TMP_DBL0);
+        bank ^= 1;
+        post(i & 1, 1);
+      }
+    } else if (i < 61) {
+      const int s = i + 1, r = s & 1;
+      fp2_t l0, l1, l3;
+      if (tmp_add_at(s)) {
+        ln(r, 0, &l0, &l1, &l3);
+        x = o.mul_line(x, l0, l1, l3);
+      }
+      x = o.sqr(x);
+      ln(r, 1, &l0, &l1, &l3);
       x = o.mul_line(x, l0, l1, l3);
     }
-    x = o.sqr(x);
-    run(bank ? TMP_DBL1 : TMP_DBL0);
-    bank ^= 1;
-    l0 = fp2_t{Sm[TMP_S_L0], Sm[TMP_S_L0 + 1]};
-    l1 = fp2_t{Sm[TMP_S_L1], Sm[TMP_S_L1 + 1]};
-    l3 = fp2_t{Sm[TMP_S_L3], Sm[TMP_S_L3 + 1]};
-    x = o.mul_line(x, l0, l1, l3);
+    __syncthreads();
   }
-  x = o.conj(x);
-  if (lane < BGV_TEAM_COMPS) {
-    fp12_t* dst = set_pair ? f + uu : (rsig ? fsig + j : gpair + j);
-    reinterpret_cast<fp_t*>(dst)[tm_fp_index(lane)] = live ? x : (lane == 0 ? fp_one() : fp_zero());
+  if (w == 1) {
+    x = o.conj(x);
+    if (lane < BGV_TEAM_COMPS) {
+      fp12_t* dst = set_pair ? f + uu : (rsig ? fsig + j : gpair + j);
+      reinterpret_cast<fp_t*>(dst)[tm_fp_index(lane)] = live ? x : (lane == 0 ? fp_one() : fp_zero());
+    }
   }
 }
 
@@ -251,7 +285,7 @@ bool bgv_sig_pairs(const bgv_dev_batch& b) {
 static void launch_miller_latency(const bgv_dev_batch& b, uint32_t nslots, uint32_t ngroups, hipStream_t st) {
   const uint32_t total = nslots + ngroups;
   if (total <= BGV_MILLER_WIDE_MAX)
-    hipLaunchKernelGGL(k_miller_wide, dim3(total), dim3(64), 0, st, b.slots, nslots, b.rpk, b.h, b.sig_status,
+    hipLaunchKernelGGL(k_miller_wide, dim3(total), dim3(128), 0, st, b.slots, nslots, b.rpk, b.h, b.sig_status,
                        b.pk_status, b.f, ngroups, b.gsum, b.gpair, static_cast<const g2_jac*>(nullptr),
                        static_cast<fp12_t*>(nullptr));
   else
@@ -275,7 +309,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
   if (bgv_sig_pairs(b)) {  // no group sums: every slot's own signature pair beside its set pair
-    hipLaunchKernelGGL(k_miller_wide, dim3(2 * n), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
+    hipLaunchKernelGGL(k_miller_wide, dim3(2 * n), dim3(128), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
                        b.pk_status, b.f, n, b.gsum, b.gpair, b.rsig, b.fsig);
     BGV_MARK(3);
     return hipGetLastError();

@@ -62,15 +62,34 @@ struct tm_dev_ops_t {
 };
 using tm_dev_ops = tm_dev_ops_t<BGV_TEAM>;
 
+// Synchronization of one wavefront's LDS exchange when the block holds other waves that run
+// their own work (k_miller_wide): the fences of __syncthreads (the LDS stores complete, no
+// compiler reordering across it) without the block barrier.  LDS operations of one wave are
+// performed in order, so the wave's later reads see its earlier stores.  In a single-wave
+// block this is what __syncthreads compiles to.
+__device__ __forceinline__ void bgv_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // One Fp12 value per 64-lane block with the wide products (bls_team.h tm_mul_part): lane l
 // holds coefficient c = l % 12 (replicated over q = l / 12); lanes q < 4 (l < 48) each compute
 // a quarter of the double-width products of their coefficient, lanes 48..63 only keep the
-// barriers.  A: 12 operand slots, B: 12, P: 4 x 12 part slots (LDS).
-struct tm_wide_ops {
+// barriers.  A: 12 operand slots, B: 12, P: 4 x 12 part slots (LDS).  WAVE: the value lives in
+// one wave of a larger block, which synchronizes on its own (bgv_wave_sync).
+template <bool WAVE>
+struct tm_wide_ops_t {
   fp_t* A;
   fp_t* B;
   fp_t* P;
   int c, q;
+  __device__ void sync() {
+    if (WAVE)
+      bgv_wave_sync();
+    else
+      __syncthreads();
+  }
   __device__ fp_t gather() {
     return tm_sum4(P[c], P[BGV_TEAM_COMPS + c], P[2 * BGV_TEAM_COMPS + c], P[3 * BGV_TEAM_COMPS + c]);
   }
@@ -79,32 +98,32 @@ struct tm_wide_ops {
       A[c] = x;
       B[c] = y;
     }
-    __syncthreads();
+    sync();
     if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_part(c, q, A, B);
-    __syncthreads();
+    sync();
     return gather();
   }
   __device__ fp_t sqr(const fp_t& x) {
     if (q == 0) A[c] = x;
-    __syncthreads();
+    sync();
     if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_sqr_part(c, q, A);
-    __syncthreads();
+    sync();
     return gather();
   }
   __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
     if (q == 0) A[c] = x;
-    __syncthreads();
+    sync();
     if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_line_part(c, q, A, l0, l1, l3);
-    __syncthreads();
+    sync();
     return gather();
   }
   __device__ fp_t line(const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) { return tm_line_lane(c, l0, l1, l3); }
   __device__ fp_t conj(const fp_t& x) { return fp_select(((c >> 1) & 1) != 0, x, fp_neg(x)); }
   __device__ fp_t frob(const fp_t& x) {
     if (q == 0) A[c] = x;
-    __syncthreads();
+    sync();
     const fp_t x0 = A[c & ~1], x1 = A[c | 1];
-    __syncthreads();
+    sync();
     return tm_frob_lane(c, x0, x1, kTeamFrob1[tm_tower_pos(c)]);
   }
   __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(c)]); }
@@ -113,5 +132,4 @@ struct tm_wide_ops {
     return __ballot(bad) == 0;  // the whole block holds one value
   }
 };
-
-
+using tm_wide_ops = tm_wide_ops_t<false>;

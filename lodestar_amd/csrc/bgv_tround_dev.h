@@ -3,7 +3,9 @@
 // c + 16 q, each computing part q of its products (tmp_lane_part: at most one product and
 // one reduction) into LDS; after a barrier lane q = 0 sums the parts into the output slot.
 // Per round a lane waits one product + one reduction instead of T products + one reduction
-// on a 16-lane team.  Host emulation: bgv_tmiller.h tmp_host_wide().
+// on a 16-lane team.  The engine is one wavefront and synchronizes on its own
+// (bgv_wave_sync), so a block may run other work on its other waves (k_miller_wide).
+// Host emulation: bgv_tmiller.h tmp_host_wide().
 #pragma once
 #include "bgv_team_dev.h"
 #include "bgv_tmiller.h"
@@ -23,9 +25,9 @@ struct tr_wide_engine {
       const int rb = tmp_rec_bytes(T, M);
       const uint8_t* rec = prog + pos + c * rb;
       P[q * BGV_TEAM + c] = tmp_lane_part(S, rec, T, M, q);
-      __syncthreads();
+      bgv_wave_sync();
       if (q == 0) S[rec[0]] = tm_sum4(P[c], P[BGV_TEAM + c], P[2 * BGV_TEAM + c], P[3 * BGV_TEAM + c]);
-      __syncthreads();
+      bgv_wave_sync();
       pos += BGV_TEAM * rb;
     }
   }
