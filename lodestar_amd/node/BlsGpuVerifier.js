@@ -29,7 +29,8 @@ const MAX_SIGNATURE_SETS_PER_JOB = 128; // index.ts:39
 // queue's 64 sets are in it; at 64 every batch waited for the timer.  Measured with 64
 // concurrent one-set callers on one MI355X (tests/node/gossip_bench.js,
 // profiles/r03/gossip/flush_at_callers.jsonl): 63 / 1 ms 11.6k sets/s at p50 5.4 ms,
-// 64 / 1 ms 9.9k at 6.4 ms, 32 / 100 ms 6.2k at 10.3 ms.
+// 64 / 1 ms 9.9k at 6.4 ms, 32 / 100 ms 6.2k at 10.3 ms (14.2k at 4.4 ms for 63 / 1 ms with
+// the later device chain, profiles/r03/gossip/two_wave_miller.jsonl).
 const MAX_BUFFERED_SIGS = 63;
 const MAX_BUFFER_WAIT_MS = 1;
 
