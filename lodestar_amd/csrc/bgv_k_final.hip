@@ -119,8 +119,8 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
 // multiplies the group's slots t, t + 8, ... (team 0 also the signature pair), the eight
 // partial products meet in LDS in a three-level tree (an eighth of k_final's serial product
 // chain).  The final exponentiation then runs on the
-// whole block with each coefficient's products split over four lanes (tm_wide_ops): 2 + 1
-// double-width products per lane and squaring instead of 7 + 1.
+// whole block with each coefficient's products split over eight lanes (tm_wide_ops_t<false, 8>):
+// one double-width product per lane for a squaring (two for a product) instead of 7 on one.
 #define BGV_FOLD_TEAMS 8  // 16-lane teams of k_final_fold's 128-thread block
 __global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                        const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict
                                        const fp12_t* __restrict__ fsig) {
   __shared__ fp_t lds[BGV_FOLD_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FOLD_TEAMS][BGV_TEAM_COMPS];
-  __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[4 * BGV_TEAM_COMPS];
+  __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[8 * BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
   const uint32_t gi = blockIdx.x;
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict
   if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
   __syncthreads();
   const int wc = threadIdx.x % BGV_TEAM_COMPS, wq = threadIdx.x / BGV_TEAM_COMPS;
-  tm_wide_ops ow{WA, WB, WP, wc, wq};
+  tm_wide_ops_t<false, 8> ow{WA, WB, WP, wc, wq};
   const fp_t xw = W[wc];
   const int wfi = tm_fp_index(wc);
   const fp_t u = tm_final_exp_u(ow, xw);

@@ -76,9 +76,11 @@ __device__ __forceinline__ void bgv_wave_sync() {
 // One Fp12 value per 64-lane block with the wide products (bls_team.h tm_mul_part): lane l
 // holds coefficient c = l % 12 (replicated over q = l / 12); lanes q < 4 (l < 48) each compute
 // a quarter of the double-width products of their coefficient, lanes 48..63 only keep the
-// barriers.  A: 12 operand slots, B: 12, P: 4 x 12 part slots (LDS).  WAVE: the value lives in
-// one wave of a larger block, which synchronizes on its own (bgv_wave_sync).
-template <bool WAVE>
+// barriers.  A: 12 operand slots, B: 12, P: NP x 12 part slots (LDS).  WAVE: the value lives in
+// one wave of a larger block, which synchronizes on its own (bgv_wave_sync).  NP = 8: the
+// eight-part products (bls_team.h tm_mul_part8 ...), one double-width product per lane for a
+// squaring or a line product, on a block of >= 96 lanes (k_final_fold).
+template <bool WAVE, int NP = 4>
 struct tm_wide_ops_t {
   fp_t* A;
   fp_t* B;
@@ -91,6 +93,11 @@ struct tm_wide_ops_t {
       __syncthreads();
   }
   __device__ fp_t gather() {
+    if (NP == 8) {
+      fp_t x[8];
+      BGV_UNROLL for (int k = 0; k < 8; ++k) x[k] = P[k * BGV_TEAM_COMPS + c];
+      return tm_sum8(x);
+    }
     return tm_sum4(P[c], P[BGV_TEAM_COMPS + c], P[2 * BGV_TEAM_COMPS + c], P[3 * BGV_TEAM_COMPS + c]);
   }
   __device__ fp_t mul(const fp_t& x, const fp_t& y) {
@@ -99,21 +106,23 @@ struct tm_wide_ops_t {
       B[c] = y;
     }
     sync();
-    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_part(c, q, A, B);
+    if (q < NP) P[q * BGV_TEAM_COMPS + c] = NP == 8 ? tm_mul_part8(c, q, A, B) : tm_mul_part(c, q, A, B);
     sync();
     return gather();
   }
   __device__ fp_t sqr(const fp_t& x) {
     if (q == 0) A[c] = x;
     sync();
-    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_sqr_part(c, q, A);
+    if (q < NP) P[q * BGV_TEAM_COMPS + c] = NP == 8 ? tm_sqr_part8(c, q, A) : tm_sqr_part(c, q, A);
     sync();
     return gather();
   }
   __device__ fp_t mul_line(const fp_t& x, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
     if (q == 0) A[c] = x;
     sync();
-    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_mul_line_part(c, q, A, l0, l1, l3);
+    if (q < NP)
+      P[q * BGV_TEAM_COMPS + c] =
+          NP == 8 ? tm_mul_line_part8(c, q, A, l0, l1, l3) : tm_mul_line_part(c, q, A, l0, l1, l3);
     sync();
     return gather();
   }

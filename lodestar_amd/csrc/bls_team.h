@@ -220,11 +220,111 @@ BGV_HD fp_t tm_mul_line_part(int c, int q, const fp_t* A, const fp2_t& l0, const
   return wide_redc(t);
 }
 
+// Eight-part forms for a block of >= 96 lanes (k_final_fold): every double-width product of
+// a coefficient on a lane of its own where the four-part forms pair them up.  mul: part q < 6
+// the two products of a_q b_j (q = 6, 7 multiply zeros); sqr: parts 2p, 2p + 1 the two
+// products of pair p of tm_sqr_part, part 6 the diagonal, part 7 zeros; mul_line: parts 2t,
+// 2t + 1 the two products of line term t.  Same products as the four-part forms, regrouped.
+BGV_HD fp_t tm_mul_part8(int c, int q, const fp_t* A, const fp_t* B) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  const bool live = q < 6;
+  const int i = live ? q : 0;
+  const bool wrap = i > k;
+  const int j = wrap ? k + 6 - i : k - i;
+  const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+  const fp_t y0 = B[2 * j], y1 = B[2 * j + 1];
+  const fp_t d = fp_sub_nr(y0, y1);
+  const fp_t s = fp_add_norm(y0, y1);
+  const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+  const fp_t X2 = fp_select(e != 0, x1n, x1);
+  const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+  const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+  const fp_t z = fp_zero();
+  wide_mac(t, live ? x0 : z, Y1);
+  wide_mac(t, live ? X2 : z, Y2);
+  return wide_redc(t);
+}
+
+BGV_HD fp_t tm_sqr_part8(int c, int q, const fp_t* A) {
+  const int k = c >> 1, e = c & 1;
+  const uint32_t kI[6] = {0x321, 0x320, 0x430, 0x410, 0x510, 0x210};
+  const uint32_t kJ[6] = {0x345, 0x451, 0x452, 0x523, 0x534, 0x345};
+  const uint32_t kW[6] = {0x7, 0x6, 0x6, 0x4, 0x4, 0x0};
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  const int p = q < 6 ? q >> 1 : 0;
+  const int i = (kI[k] >> (4 * p)) & 0xf, j = (kJ[k] >> (4 * p)) & 0xf;
+  const bool wrap = (kW[k] >> p) & 1;
+  const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+  const fp_t y0 = A[2 * j], y1 = A[2 * j + 1];
+  const fp_t d = fp_sub_nr(y0, y1);
+  const fp_t s = fp_add_norm(y0, y1);
+  const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+  const fp_t X2n = fp_select(e != 0, x1n, x1);
+  const bool cross = i != j;
+  const fp_t X1 = fp_select(cross, x0, fp_add_norm(x0, x0));
+  const fp_t X2 = fp_select(cross, X2n, fp_add_norm(X2n, X2n));
+  const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y0, y1);
+  const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y1, y0);
+  const int h = k >> 1;
+  const fp_t h0 = A[2 * h], h1 = A[2 * h + 1];
+  const bool even = (k & 1) == 0;
+  const fp_t Pd = e ? fp_add_norm(h0, h0) : fp_add_norm(h0, h1);
+  const fp_t Qd = e ? h1 : fp_sub_nr(h0, h1);
+  const fp_t z = fp_zero();
+  const fp_t X = q < 6 ? ((q & 1) ? X2 : X1) : (q == 6 && even ? Pd : z);
+  const fp_t Y = q < 6 ? ((q & 1) ? Y2 : Y1) : Qd;
+  wide_mac(t, X, Y);
+  return wide_redc(t);
+}
+
+BGV_HD fp_t tm_mul_line_part8(int c, int q, const fp_t* A, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+  const int k = c >> 1, e = c & 1;
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  const int term = q < 6 ? q >> 1 : 0;
+  const int j = term == 0 ? 0 : term + 1;  // 0, 2, 3
+  const fp2_t& y = term == 0 ? l0 : (term == 1 ? l1 : l3);
+  const bool wrap = k < j;
+  const int i = wrap ? k - j + 6 : k - j;
+  const fp_t x0 = A[2 * i], x1 = A[2 * i + 1];
+  const fp_t d = fp_sub_nr(y.c0, y.c1);
+  const fp_t s = fp_add_norm(y.c0, y.c1);
+  const fp_t x1n = fp_sub_nr(fp_zero(), x1);
+  const fp_t X2 = fp_select(e != 0, x1n, x1);
+  const fp_t Y1 = wrap ? fp_select(e != 0, d, s) : fp_select(e != 0, y.c0, y.c1);
+  const fp_t Y2 = wrap ? fp_select(e != 0, s, d) : fp_select(e != 0, y.c1, y.c0);
+  const fp_t z = fp_zero();
+  wide_mac(t, q < 6 ? ((q & 1) ? X2 : x0) : z, (q & 1) ? Y2 : Y1);
+  return wide_redc(t);
+}
+
 // sum of the four parts of a coefficient, back below 2p
 BGV_HD fp_t tm_sum4(const fp_t& a, const fp_t& b, const fp_t& c, const fp_t& d) {
   fp_t r;
   BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i] + c.v[i] + d.v[i];
   // value < 8p, limbs < 2^30: one signed chain subtracting q p, q from the top limb (lz_out)
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  const uint32_t qt = r.v[NL - 1] / (uint32_t)(P_[NL - 1] + 1);
+  int64_t cy = 0;
+  fp_t o;
+  BGV_UNROLL for (int i = 0; i < NL - 1; ++i) {
+    const int64_t s = (int64_t)r.v[i] - (int64_t)((uint64_t)qt * P_[i]) + cy;
+    o.v[i] = (uint32_t)s & LMASK;
+    cy = s >> LBITS;
+  }
+  o.v[NL - 1] = (uint32_t)((int64_t)r.v[NL - 1] - (int64_t)((uint64_t)qt * P_[NL - 1]) + cy);
+  return o;
+}
+
+// sum of the eight parts of a coefficient (each < 1.07 p, limbs < 2^28.1), back below 2p by
+// the same one-chain subtraction of qt p (value < 8.6 p, limbs < 2^31.2)
+BGV_HD fp_t tm_sum8(const fp_t* x) {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i)
+    r.v[i] = x[0].v[i] + x[1].v[i] + x[2].v[i] + x[3].v[i] + x[4].v[i] + x[5].v[i] + x[6].v[i] + x[7].v[i];
   const uint32_t P_[NL] = BGV_P_LIMBS;
   const uint32_t qt = r.v[NL - 1] / (uint32_t)(P_[NL - 1] + 1);
   int64_t cy = 0;
@@ -428,6 +528,29 @@ struct tm_emu_wide_ops : tm_emu_ops {
       r.c[c] = tm_sum4(tm_mul_line_part(c, 0, a.c, l0, l1, l3), tm_mul_line_part(c, 1, a.c, l0, l1, l3),
                        tm_mul_line_part(c, 2, a.c, l0, l1, l3), tm_mul_line_part(c, 3, a.c, l0, l1, l3));
     return r;
+  }
+};
+
+// the eight-part products (tm_mul_part8 / tm_sqr_part8 / tm_mul_line_part8), lane by lane
+struct tm_emu_wide8_ops : tm_emu_ops {
+  template <class F>
+  BGV_HD tm_emu_t gather8(F part) {
+    tm_emu_t r;
+    for (int c = 0; c < BGV_TEAM_COMPS; ++c) {
+      fp_t x[8];
+      for (int q = 0; q < 8; ++q) x[q] = part(c, q);
+      r.c[c] = tm_sum8(x);
+    }
+    return r;
+  }
+  BGV_HD tm_emu_t mul(const tm_emu_t& a, const tm_emu_t& b) {
+    return gather8([&](int c, int q) { return tm_mul_part8(c, q, a.c, b.c); });
+  }
+  BGV_HD tm_emu_t sqr(const tm_emu_t& a) {
+    return gather8([&](int c, int q) { return tm_sqr_part8(c, q, a.c); });
+  }
+  BGV_HD tm_emu_t mul_line(const tm_emu_t& a, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
+    return gather8([&](int c, int q) { return tm_mul_line_part8(c, q, a.c, l0, l1, l3); });
   }
 };
 

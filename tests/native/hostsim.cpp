@@ -233,6 +233,19 @@ int hs_team_final_is_one_wide(const uint8_t* f) {
   tm_emu_wide_ops o;
   return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
 }
+// the eight-part products of k_final_fold's final exponentiation
+void hs_team_mul_wide8(uint8_t* r, const uint8_t* a, const uint8_t* b) {
+  tm_emu_wide8_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul(tm_emu_from_fp12(in_fp12(a)), tm_emu_from_fp12(in_fp12(b)))));
+}
+void hs_team_sqr_wide8(uint8_t* r, const uint8_t* a) {
+  tm_emu_wide8_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.sqr(tm_emu_from_fp12(in_fp12(a)))));
+}
+int hs_team_final_is_one_wide8(const uint8_t* f) {
+  tm_emu_wide8_ops o;
+  return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
+}
 // Q handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
 static g2_jac jac_scaled(const g2_aff& a) {
   const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};
@@ -292,6 +305,10 @@ void hs_team_mul_line(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uin
 }
 void hs_team_mul_line_wide(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
   tm_emu_wide_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.mul_line(tm_emu_from_fp12(in_fp12(f)), in_fp2(l0), in_fp2(l1), in_fp2(l3))));
+}
+void hs_team_mul_line_wide8(uint8_t* r, const uint8_t* f, const uint8_t* l0, const uint8_t* l1, const uint8_t* l3) {
+  tm_emu_wide8_ops o;
   out_fp12(r, tm_emu_to_fp12(o.mul_line(tm_emu_from_fp12(in_fp12(f)), in_fp2(l0), in_fp2(l1), in_fp2(l3))));
 }
 // one set through the device equation: k_prep (r pk affine, r sig Jacobian), k_miller

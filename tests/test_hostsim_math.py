@@ -357,6 +357,8 @@ def test_team_mul_line(L):
         assert got.raw == want.raw
         L.hs_team_mul_line_wide(got, f, l0, l1, l3)  # four parts per coefficient (k_miller_wide)
         assert got.raw == want.raw
+        L.hs_team_mul_line_wide8(got, f, l0, l1, l3)  # eight parts per coefficient
+        assert got.raw == want.raw
 
 
 def test_verify_one_blst_equation(L):
@@ -388,10 +390,14 @@ def test_team_fp12_ops(L):
         assert got.raw == want.raw
         L.hs_team_mul_wide(got, a, b)  # four parts per coefficient (latency-path closing)
         assert got.raw == want.raw
+        L.hs_team_mul_wide8(got, a, b)  # eight parts per coefficient (k_final_fold)
+        assert got.raw == want.raw
         L.hs_fp12_sqr(want, a)
         L.hs_team_sqr(got, a)  # 7-product team squaring
         assert got.raw == want.raw
         L.hs_team_sqr_wide(got, a)
+        assert got.raw == want.raw
+        L.hs_team_sqr_wide8(got, a)
         assert got.raw == want.raw
         for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
             tf(got, a)
@@ -409,6 +415,7 @@ def test_team_final_exp_check(L):
         assert L.hs_final_is_one(f) == 0
         assert L.hs_team_final_is_one(f) == 0
         assert L.hs_team_final_is_one_wide(f) == 0
+        assert L.hs_team_final_is_one_wide8(f) == 0
     p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
     q = g2_rand_in_group()
     # e(P, Q) e(-P, Q) == 1 and e(P, Q) e(-P, Q2) != 1 (Miller values multiplied)
@@ -419,9 +426,11 @@ def test_team_final_exp_check(L):
     assert L.hs_final_is_one(m.raw) == 1
     assert L.hs_team_final_is_one(m.raw) == 1
     assert L.hs_team_final_is_one_wide(m.raw) == 1
+    assert L.hs_team_final_is_one_wide8(m.raw) == 1
     q2 = g2_rand_in_group()
     L.hs_miller_loop(b, hs.g1_b(o.g1_neg(p)), hs.g2_b(q2))
     L.hs_fp12_mul(m, a.raw, b.raw)
     assert L.hs_final_is_one(m.raw) == 0
     assert L.hs_team_final_is_one(m.raw) == 0
     assert L.hs_team_final_is_one_wide(m.raw) == 0
+    assert L.hs_team_final_is_one_wide8(m.raw) == 0
