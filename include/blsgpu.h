@@ -114,7 +114,12 @@ int bgv_destroy(bgv_ctx* ctx);
  * the beacon state) or BGV_PK_UNCOMPRESSED (96 bytes).  Keys are trusted: decoded
  * without a subgroup check, as Index2PubkeyCache does
  * (state-transition/src/cache/pubkeyCache.ts:56-77, epochContext.ts:702-705).
- * Returns BGV_OK, or -code of the first undecodable key. */
+ * Appending (first_index == bgv_pubkeys_count) does not wait for running verifies: the keys
+ * are decoded into staging memory and published once every device holds them.  A gap
+ * (first_index > count) returns -BGV_E_ARG and writes nothing.  Undecodable records do not
+ * stop the run: every index of it is committed, the undecodable ones are marked (a set that
+ * names one rejects with BGV_E_BAD_INDEX) and -code of the first undecodable key is
+ * returned; a later put over the same index replaces the mark. */
 int bgv_pubkeys_put(bgv_ctx* ctx, uint32_t first_index, const uint8_t* keys, size_t n, int fmt);
 size_t bgv_pubkeys_count(const bgv_ctx* ctx);
 

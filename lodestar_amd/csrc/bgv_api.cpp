@@ -33,6 +33,7 @@
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <unordered_set>
 #include <thread>
 #include <vector>
 
@@ -393,7 +394,15 @@ struct Call {
 
 struct bgv_ctx {
   std::vector<Device> devs;
-  size_t n_pubkeys = 0;
+  // cached pubkeys: entries [0, n_pubkeys) are valid on every device.  A pure append writes
+  // entries at and past n_pubkeys (which no submitted call reads) and then publishes the new
+  // count, so it needs only the shared cache_mu; growth and overwrites take it exclusively.
+  std::atomic<size_t> n_pubkeys{0};
+  std::mutex put_mu;  // one cache writer at a time (bgv_pubkeys_put, bgv_keygen)
+  // indices whose record failed to decode in bgv_pubkeys_put: kept in the count (later runs
+  // stay contiguous) but any set naming one rejects with BGV_E_BAD_INDEX.  Written under the
+  // exclusive cache_mu, read under the shared one.
+  std::unordered_set<uint32_t> bad_pk;
   std::atomic<bool> closed{false};
   std::mutex rng_mu;
   uint64_t rng_seed = 0, rng_state = 0;
@@ -473,7 +482,7 @@ static int exec_reserve_slots(Exec& x, uint32_t slots) {
   if (x.d_slots) (void)hipFree(x.d_slots);
   x.slot_mem = nullptr;
   x.d_slots = nullptr;
-  HIPCHK(hipMalloc(&x.slot_mem, bgv_slot_bytes() * n));
+  HIPCHK(hipMalloc(&x.slot_mem, bgv_slot_mem_bytes(n)));
   HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_slots), sizeof(bgv_dslot) * n));
   x.slot_cap = n;
   return BGV_OK;
@@ -630,7 +639,7 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
           return -BGV_E_ARG;
         else if (s.pk_indices)
           for (uint32_t q = 0; q < s.n_pk; ++q)
-            if (s.pk_indices[q] >= c->n_pubkeys) {
+            if (s.pk_indices[q] >= c->n_pubkeys || (!c->bad_pk.empty() && c->bad_pk.count(s.pk_indices[q]))) {
               call->code[j] = -BGV_E_BAD_INDEX;
               break;
             }
@@ -1272,7 +1281,13 @@ static void retry_loop(bgv_ctx* c, Device* d) {
       s.rq.pop_front();
     }
     job.x->close = s.retry;
+    // No cache_mu here: the retry kernels (k_gsum, the group pairs, the closing) read only the
+    // per-slot results of pass 1 (r_i sig_i, f_i, u values), never the pubkey cache, and
+    // bgv_close joins this thread before it frees the devices.  A batch in its retry rounds
+    // keeps the device busy, so it counts as running for the coalescing window.
+    c->running.fetch_add(1);
     const int rc = run_retries(c, *d, *job.x, job.calls, *job.st);
+    c->running.fetch_sub(1);
     finish_calls(job.calls, rc);
     exec_release(*d, job.x);
   }
@@ -1466,7 +1481,7 @@ int bgv_set_rng_seed(bgv_ctx* c, uint64_t seed) {
   return BGV_OK;
 }
 
-size_t bgv_pubkeys_count(const bgv_ctx* c) { return c ? c->n_pubkeys : 0; }
+size_t bgv_pubkeys_count(const bgv_ctx* c) { return c ? c->n_pubkeys.load() : 0; }
 
 // grow every device's cache to hold `need` entries (contents preserved); caller holds cache_mu exclusively
 static int cache_reserve(bgv_ctx* c, size_t need) {
@@ -1488,45 +1503,121 @@ static int cache_reserve(bgv_ctx* c, size_t need) {
   return BGV_OK;
 }
 
+// Decode n records into per-device staging buffers (the slow part: host-to-device copy and
+// one square root per compressed key) under the SHARED cache lock, so running and newly
+// submitted verifies are never held up by it; then commit.  A pure append within capacity
+// copies the staged entries past n_pubkeys and publishes the new count, still under the shared
+// lock; growth, overwrites and undecodable records commit under the exclusive lock (rare: the
+// capacity doubles, validator indices only grow).  Records that fail to decode are committed
+// as marked indices (sets naming them reject with BGV_E_BAD_INDEX) and the first one's code is
+// returned, so one bad key neither leaves a hole that blocks later appends nor reaches a
+// verify as a usable key.
 int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, int fmt) {
   if (!c || (n && !keys) || (fmt != BGV_PK_COMPRESSED && fmt != BGV_PK_UNCOMPRESSED)) return -BGV_E_ARG;
-  std::unique_lock<std::shared_mutex> lk(c->cache_mu);
-  if (c->closed) return -BGV_E_CLOSED;
-  if ((size_t)first > c->n_pubkeys) return -BGV_E_ARG;  // append or overwrite, no holes
-  if (n == 0) return BGV_OK;
-  const size_t need = (size_t)first + n;
+  std::lock_guard<std::mutex> plk(c->put_mu);
   const size_t esz = bgv_cache_entry_bytes();
-  int first_err = BGV_OK;
+  std::vector<void*> staged(c->devs.size(), nullptr);
+  std::vector<int32_t> status(n, 0);
+  auto free_staged = [&] {
+    for (size_t di = 0; di < staged.size(); ++di)
+      if (staged[di]) {
+        (void)hipSetDevice(c->devs[di].id);
+        (void)hipFree(staged[di]);
+      }
+  };
   {
-    int rc = cache_reserve(c, need);
-    if (rc) return rc;
-  }
-  for (Device& d : c->devs) {
-    HIPCHK(hipSetDevice(d.id));
-    const size_t chunk = 1 << 20;
-    uint8_t* dk = nullptr;
-    int32_t* dst = nullptr;
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&dk), (size_t)fmt * std::min(n, chunk) + 1));
-    HIPCHK(hipMalloc(reinterpret_cast<void**>(&dst), 4 * std::min(n, chunk) + 4));
-    std::vector<int32_t> hst;
-    for (size_t off = 0; off < n; off += chunk) {
-      const size_t m = std::min(chunk, n - off);
-      HIPCHK(hipMemcpyAsync(dk, keys + (size_t)fmt * off, (size_t)fmt * m, hipMemcpyHostToDevice, d.stream));
-      bgv_cache_entry* dst_cache =
-          reinterpret_cast<bgv_cache_entry*>(reinterpret_cast<uint8_t*>(d.cache) + esz * (first + off));
-      HIPCHK(bgv_launch_cache_put(dk, (uint32_t)m, fmt, dst_cache, dst, d.stream));
-      hst.resize(m);
-      HIPCHK(hipMemcpyAsync(hst.data(), dst, 4 * m, hipMemcpyDeviceToHost, d.stream));
-      HIPCHK(hipStreamSynchronize(d.stream));
-      for (size_t i = 0; i < m && first_err == BGV_OK; ++i)
-        if (hst[i]) first_err = hst[i];
+    std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+    if (c->closed) return -BGV_E_CLOSED;
+    if ((size_t)first > c->n_pubkeys) return -BGV_E_ARG;  // append or overwrite, no holes
+    if (n == 0) return BGV_OK;
+    std::lock_guard<std::mutex> ulk(c->util_mu);
+    for (size_t di = 0; di < c->devs.size(); ++di) {
+      Device& d = c->devs[di];
+      if (hipSetDevice(d.id) != hipSuccess || hipMalloc(&staged[di], esz * n) != hipSuccess) {
+        free_staged();
+        return -BGV_E_DEVICE;
+      }
+      const size_t chunk = 1 << 20;
+      uint8_t* dk = nullptr;
+      int32_t* dst = nullptr;
+      int rc = BGV_OK;
+      if (hipMalloc(reinterpret_cast<void**>(&dk), (size_t)fmt * std::min(n, chunk) + 1) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&dst), 4 * std::min(n, chunk) + 4) != hipSuccess)
+        rc = -BGV_E_DEVICE;
+      for (size_t off = 0; rc == BGV_OK && off < n; off += chunk) {
+        const size_t m = std::min(chunk, n - off);
+        bgv_cache_entry* out =
+            reinterpret_cast<bgv_cache_entry*>(static_cast<uint8_t*>(staged[di]) + esz * off);
+        if (hipMemcpyAsync(dk, keys + (size_t)fmt * off, (size_t)fmt * m, hipMemcpyHostToDevice, d.stream) !=
+                hipSuccess ||
+            bgv_launch_cache_put(dk, (uint32_t)m, fmt, out, dst, d.stream) != hipSuccess ||
+            (di == 0 && hipMemcpyAsync(status.data() + off, dst, 4 * m, hipMemcpyDeviceToHost, d.stream) !=
+                            hipSuccess) ||
+            hipStreamSynchronize(d.stream) != hipSuccess)
+          rc = -BGV_E_DEVICE;
+      }
+      if (dk) (void)hipFree(dk);
+      if (dst) (void)hipFree(dst);
+      if (rc) {
+        free_staged();
+        return rc;
+      }
     }
-    (void)hipFree(dk);
-    (void)hipFree(dst);
   }
-  if (first_err) return -first_err;
-  c->n_pubkeys = std::max(c->n_pubkeys, need);
-  return BGV_OK;
+  int first_err = BGV_OK;
+  std::vector<uint32_t> bad;
+  for (size_t i = 0; i < n; ++i)
+    if (status[i]) {
+      if (first_err == BGV_OK) first_err = status[i];
+      bad.push_back(first + (uint32_t)i);
+    }
+  const size_t need = (size_t)first + n;
+  auto copy_in = [&]() -> int {
+    for (size_t di = 0; di < c->devs.size(); ++di) {
+      Device& d = c->devs[di];
+      HIPCHK(hipSetDevice(d.id));
+      HIPCHK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(d.cache) + esz * first, staged[di], esz * n,
+                            hipMemcpyDeviceToDevice, d.stream));
+      HIPCHK(hipStreamSynchronize(d.stream));
+    }
+    return BGV_OK;
+  };
+  int rc = BGV_OK;
+  bool done = false;
+  {
+    std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+    if (c->closed) {
+      rc = -BGV_E_CLOSED;
+      done = true;
+    } else if (first == c->n_pubkeys && bad.empty()) {
+      bool fits = true;
+      for (const Device& d : c->devs) fits = fits && need <= d.cache_cap;
+      if (fits) {
+        std::lock_guard<std::mutex> ulk(c->util_mu);
+        rc = copy_in();
+        if (rc == BGV_OK) c->n_pubkeys.store(need);
+        done = true;
+      }
+    }
+  }
+  if (!done) {
+    std::unique_lock<std::shared_mutex> clk(c->cache_mu);
+    if (c->closed) {
+      rc = -BGV_E_CLOSED;
+    } else {
+      std::lock_guard<std::mutex> ulk(c->util_mu);
+      rc = cache_reserve(c, need);
+      if (rc == BGV_OK) rc = copy_in();
+      if (rc == BGV_OK) {
+        for (uint32_t i = first; i < need; ++i) c->bad_pk.erase(i);  // overwritten entries
+        for (uint32_t i : bad) c->bad_pk.insert(i);
+        c->n_pubkeys.store(std::max(c->n_pubkeys.load(), need));
+      }
+    }
+  }
+  free_staged();
+  if (rc) return rc;
+  return first_err ? -first_err : BGV_OK;
 }
 
 int bgv_verify(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
@@ -1640,7 +1731,7 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
     const bgv_set& st = sets[i];
     if (!st.pk_indices || st.n_pk == 0 || !st.msg || (st.sig_len && !st.sig)) return -BGV_E_ARG;
     for (uint32_t q = 0; q < st.n_pk; ++q)
-      if (st.pk_indices[q] >= c->n_pubkeys) return -BGV_E_BAD_INDEX;
+      if (st.pk_indices[q] >= c->n_pubkeys || c->bad_pk.count(st.pk_indices[q])) return -BGV_E_BAD_INDEX;
     bgv_dslot s;
     memset(&s, 0, sizeof(s));
     s.flags = BGV_SLOT_PK_CACHED;
@@ -1674,6 +1765,10 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
   Exec* x = new Exec();
   uint8_t *dh = nullptr, *df = nullptr;
   int rc = exec_create(x);
+  // a non-blocking stream of its own, like the dispatchers' (not the legacy null stream)
+  hipStream_t dstream = nullptr;
+  if (!rc && hipStreamCreateWithFlags(&dstream, hipStreamNonBlocking) != hipSuccess) rc = -BGV_E_DEVICE;
+  x->main = dstream;
   if (!rc) rc = exec_reserve_slots(*x, nslots);
   if (!rc) rc = exec_reserve_groups(*x, ngroups);
   if (!rc) rc = grow(&x->d_idx, &x->idx_cap, idx.size());
@@ -1702,7 +1797,8 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
   }
   if (dh) (void)hipFree(dh);
   if (df) (void)hipFree(df);
-  exec_destroy(x);
+  exec_destroy(x);  // synchronizes x->main first
+  if (dstream) (void)hipStreamDestroy(dstream);
   if (rc) return rc;
   for (size_t i = 0; i < nsets; ++i) {
     out_status[2 * i] = ss[i];
@@ -1717,7 +1813,7 @@ int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out
   std::shared_lock<std::shared_mutex> clk(c->cache_mu);
   if (c->closed) return -BGV_E_CLOSED;
   for (size_t i = 0; i < n; ++i)
-    if (idx[i] >= c->n_pubkeys) return -BGV_E_BAD_INDEX;
+    if (idx[i] >= c->n_pubkeys || c->bad_pk.count(idx[i])) return -BGV_E_BAD_INDEX;
   std::lock_guard<std::mutex> lk(c->util_mu);
   Device& d = c->devs[0];
   HIPCHK(hipSetDevice(d.id));
@@ -1892,6 +1988,7 @@ int bgv_deposits_verify(bgv_ctx* c, const uint8_t* keys48, const uint8_t* msgs32
 
 int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, uint8_t* out48) {
   if (!c || (n && !sks)) return -BGV_E_ARG;
+  std::lock_guard<std::mutex> plk(c->put_mu);
   std::unique_lock<std::shared_mutex> clk(c->cache_mu);
   if (c->closed) return -BGV_E_CLOSED;
   if (cache_first > (int64_t)c->n_pubkeys) return -BGV_E_ARG;
@@ -1918,7 +2015,10 @@ int bgv_keygen(bgv_ctx* c, const uint8_t* sks, size_t n, int64_t cache_first, ui
     (void)hipFree(dsk);
     (void)hipFree(dout);
   }
-  if (cache_first >= 0) c->n_pubkeys = std::max(c->n_pubkeys, (size_t)cache_first + n);
+  if (cache_first >= 0) {
+    for (size_t i = 0; i < n; ++i) c->bad_pk.erase((uint32_t)(cache_first + i));
+    c->n_pubkeys.store(std::max(c->n_pubkeys.load(), (size_t)cache_first + n));
+  }
   return BGV_OK;
 }
 

@@ -197,8 +197,12 @@ __global__ void k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restric
 
 }  // extern "C"
 
-size_t bgv_slot_bytes() {
-  return 2 * sizeof(g2_jac) + sizeof(g1_jac) + 2 * sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t);
+size_t bgv_slot_bytes() { return 2 * sizeof(g2_jac) + sizeof(g1_jac) + sizeof(fp12_t) + sizeof(g1_jac) + 2 * sizeof(int32_t); }
+// the per-slot signature pairs (fsig) serve only calls of at most BGV_PREP_WIDE_MAX slots
+// (bgv_sig_pairs), so they get that many entries, not one per slot of the capacity
+static size_t fsig_slots(uint32_t cap_slots) { return std::min<size_t>(cap_slots, BGV_PREP_WIDE_MAX + 64); }
+size_t bgv_slot_mem_bytes(uint32_t cap_slots) {
+  return bgv_slot_bytes() * (size_t)cap_slots + sizeof(fp12_t) * fsig_slots(cap_slots);
 }
 size_t bgv_group_bytes() { return sizeof(g2_jac) + 3 * sizeof(fp12_t) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
@@ -214,7 +218,7 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   b->f = reinterpret_cast<fp12_t*>(p);
   p += sizeof(fp12_t) * (size_t)cap_slots;
   b->fsig = reinterpret_cast<fp12_t*>(p);
-  p += sizeof(fp12_t) * (size_t)cap_slots;
+  p += sizeof(fp12_t) * fsig_slots(cap_slots);
   b->pk_agg = reinterpret_cast<g1_jac*>(p);
   p += sizeof(g1_jac) * (size_t)cap_slots;
   b->sig_status = reinterpret_cast<int32_t*>(p);

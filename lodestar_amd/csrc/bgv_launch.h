@@ -80,6 +80,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
 size_t bgv_slot_bytes();
+size_t bgv_slot_mem_bytes(uint32_t cap_slots);  // the per-slot arrays of an Exec of cap_slots slots
 size_t bgv_group_bytes();
 size_t bgv_cache_entry_bytes();
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups);

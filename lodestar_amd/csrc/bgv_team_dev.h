@@ -136,9 +136,13 @@ struct tm_wide_ops_t {
     return tm_frob_lane(c, x0, x1, kTeamFrob1[tm_tower_pos(c)]);
   }
   __device__ fp_t frob2(const fp_t& x) { return fp_mul(x, kTeamFrob2[tm_tower_pos(c)]); }
+  // The q == 0 lanes hold the value; the flag is reduced over the whole engine (the wave, or
+  // the block with a block barrier), so every lane -- also those of a second wave, which hold
+  // no q == 0 lane -- returns the same answer.  Every lane of the engine must call it.
   __device__ bool is_fp6(const fp_t& x) {
     const bool bad = q == 0 && ((c >> 1) & 1) && !fp_is_zero(x);
-    return __ballot(bad) == 0;  // the whole block holds one value
+    if (WAVE) return __ballot(bad) == 0;
+    return __syncthreads_or(bad ? 1 : 0) == 0;
   }
 };
 using tm_wide_ops = tm_wide_ops_t<false>;

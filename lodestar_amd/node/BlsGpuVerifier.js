@@ -35,6 +35,8 @@ const MAX_BUFFERED_SIGS = 63;
 const MAX_BUFFER_WAIT_MS = 1;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
+const BGV_E_ARG = 23; // include/blsgpu.h
+const PUBKEY_RUN = 8192;
 
 class QueueError extends Error {
   constructor(code) {
@@ -90,6 +92,8 @@ class BlsGpuVerifier {
     this.metrics = modules.metrics || null;
     this.ctx = opts.ctx || addon.init(opts.devices || []);
     this.pendingPubkeys = [];
+    this.flushing = null;
+    this.onPubkeyError = opts.onPubkeyError || null;
     this.blsVerifyAllMultiThread = opts.blsVerifyAllMultiThread || false;
     this.maxBufferedSigs = opts.maxBufferedSigs || MAX_BUFFERED_SIGS;
     this.maxBufferWaitMs = opts.maxBufferWaitMs || MAX_BUFFER_WAIT_MS;
@@ -108,40 +112,77 @@ class BlsGpuVerifier {
    * state-transition's pubkey-added hook, called with (index, 48-byte pubkey, PublicKey).  It
    * tags the PublicKey with .index (so sets built by the reference's producers travel as
    * indices) and queues the key; queued keys go to the device in contiguous runs before the
-   * next verification or every 65,536 keys.
+   * next verification or every 65,536 keys, off the event loop (flushPubkeys).
    */
   pubkeyAddedHook() {
     return (index, pubkey, pk) => {
       if (pk && typeof pk === "object") pk.index = index;
       this.pendingPubkeys.push([index, pubkey]);
-      if (this.pendingPubkeys.length >= 65536) this.flushPubkeys();
+      // a gap error here reappears at the next verifySignatureSets, which awaits the flush
+      if (this.pendingPubkeys.length >= 65536) this.flushPubkeys().catch(() => {});
     };
   }
 
-  // A run leaves the queue only once the device holds it: if a put throws (e.g. a gap in the
-  // indices), that run and every later one stay queued for the next flush, and the error
-  // reaches the caller.
+  /**
+   * Uploads the queued keys in contiguous runs with the addon's asynchronous put (a libuv pool
+   * thread decodes them; the library publishes a run once every device holds it, without
+   * waiting for running verifies), so a validator-set growth never stalls the event loop
+   * (EpochContext.addPubkey, state-transition/src/cache/epochContext.ts:702-705;
+   * pubkeyCache.ts:56-77).  One flush chain at a time; keys queued meanwhile join it.
+   * A run that fails for a gap in the indices (nothing written) stays queued, with every run
+   * after it, and the error reaches the caller.  A run with undecodable records is committed
+   * with those indices marked (sets naming them reject BGV_E_BAD_INDEX): it is reported once
+   * (onPubkeyError, else a console warning) and dropped, so one bad key cannot stop later
+   * uploads or verification.
+   */
   flushPubkeys() {
-    const p = this.pendingPubkeys;
-    if (p.length === 0 || this.closed) return;
-    p.sort((a, b) => a[0] - b[0]);
-    let i = 0;
-    try {
-      while (i < p.length) {
-        let j = i + 1;
-        while (j < p.length && p[j][0] === p[j - 1][0] + 1) j++;
-        const buf = new Uint8Array(48 * (j - i));
-        for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
-        addon.pubkeysPut(this.ctx, p[i][0], buf, 48);
-        i = j;
+    if (this.closed) return Promise.resolve();
+    if (!this.flushing && this.pendingPubkeys.length) {
+      this.flushing = this._flushRuns().finally(() => {
+        this.flushing = null;
+      });
+    }
+    return this.flushing || Promise.resolve();
+  }
+
+  async _flushRuns() {
+    while (this.pendingPubkeys.length && !this.closed) {
+      const p = this.pendingPubkeys;
+      this.pendingPubkeys = [];
+      let sorted = true;
+      for (let k = 1; k < p.length && sorted; k++) sorted = p[k][0] > p[k - 1][0];
+      if (!sorted) p.sort((a, b) => a[0] - b[0]);
+      let i = 0;
+      try {
+        while (i < p.length) {
+          // contiguous runs of at most PUBKEY_RUN keys: the main thread only copies one run's
+          // bytes between awaits
+          let j = i + 1;
+          while (j < p.length && j - i < PUBKEY_RUN && p[j][0] === p[j - 1][0] + 1) j++;
+          const buf = new Uint8Array(48 * (j - i));
+          for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
+          try {
+            await addon.pubkeysPutAsync(this.ctx, p[i][0], buf, 48);
+          } catch (e) {
+            if (e.bgvCode === -BGV_E_ARG || this.closed) throw e;
+            this.reportPubkeyError(e, p[i][0], j - i);
+          }
+          i = j;
+        }
+      } finally {
+        if (i < p.length) this.pendingPubkeys = p.slice(i).concat(this.pendingPubkeys);
       }
-    } finally {
-      this.pendingPubkeys = p.slice(i);
     }
   }
 
+  reportPubkeyError(e, first, n) {
+    const msg = `BlsGpuVerifier: pubkeys [${first}, ${first + n}) uploaded with undecodable keys marked: ${e.message}`;
+    if (this.onPubkeyError) this.onPubkeyError(e, first, n);
+    else console.warn(msg);
+  }
+
   async verifySignatureSets(sets, opts = {}) {
-    this.flushPubkeys();
+    if (this.pendingPubkeys.length || this.flushing) await this.flushPubkeys();
     const nAgg = getAggregatedPubkeysCount(sets);
     this.counters.aggregatedPubkeys += nAgg;
     if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(nAgg);

@@ -15,6 +15,7 @@
  *
  *   init(devices?: number[]) -> ctx
  *   pubkeysPut(ctx, firstIndex, keys: Uint8Array, fmt: 48 | 96)
+ *   pubkeysPutAsync(ctx, firstIndex, keys, fmt) -> Promise<void>  (on a libuv pool thread)
  *   keygen(ctx, sks: Uint8Array, cacheFirst: number) -> Uint8Array (48-B pubkeys)
  *   sign(ctx, sks: Uint8Array, msgs: Uint8Array) -> Uint8Array (96-B signatures)
  *   verify(ctx, jobs: {sets: {pkIndices: Uint32Array | pkBytes: Uint8Array (n x 96),
@@ -203,6 +204,81 @@ static napi_value js_pubkeys_put(napi_env env, napi_callback_info info) {
   int rc = bgv_pubkeys_put(ctx, first, keys, len / (size_t)fmt, fmt);
   if (rc) return throw_code(env, rc);
   return NULL;
+}
+
+/* pubkeysPutAsync(ctx, firstIndex, keys, fmt) -> Promise<void>: bgv_pubkeys_put on a libuv pool
+ * thread, so a validator-set growth (EpochContext.addPubkey, epochContext.ts:702-705) never
+ * blocks the event loop; the library decodes into staging memory without holding up running
+ * verifies.  Rejects with an Error whose .bgvCode is the negative library code (-BGV_E_ARG for
+ * a gap in the indices: nothing was written; a BLST code: the run was committed with the
+ * undecodable indices marked). */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref ctx_ref, keys_ref;
+  bgv_ctx* c;
+  uint32_t first;
+  const uint8_t* keys;
+  size_t n;
+  int fmt, rc;
+} put_req;
+
+static void put_execute(napi_env env, void* data) {
+  (void)env;
+  put_req* r = (put_req*)data;
+  r->rc = bgv_pubkeys_put(r->c, r->first, r->keys, r->n, r->fmt);
+}
+
+static void put_complete(napi_env env, napi_status status, void* data) {
+  put_req* r = (put_req*)data;
+  if (status == napi_ok && r->rc == 0) {
+    napi_value undef;
+    napi_get_undefined(env, &undef);
+    napi_resolve_deferred(env, r->deferred, undef);
+  } else {
+    const int rc = status == napi_ok ? r->rc : -BGV_E_ARG;
+    napi_value msg, err, code;
+    napi_create_string_utf8(env, bgv_strerror(rc), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_create_int32(env, rc, &code);
+    napi_set_named_property(env, err, "bgvCode", code);
+    napi_reject_deferred(env, r->deferred, err);
+  }
+  napi_delete_reference(env, r->ctx_ref);
+  napi_delete_reference(env, r->keys_ref);
+  napi_delete_async_work(env, r->work);
+  free(r);
+}
+
+static napi_value js_pubkeys_put_async(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4], promise, name;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  OPEN_CTX(env, argv[0], ctx);
+  uint8_t* keys;
+  size_t len;
+  uint32_t first = 0;
+  int32_t fmt = 48;
+  napi_get_value_uint32(env, argv[1], &first);
+  if (get_bytes(env, argv[2], &keys, &len)) return throw_code(env, -BGV_E_ARG);
+  napi_get_value_int32(env, argv[3], &fmt);
+  if (fmt != 48 && fmt != 96) return throw_code(env, -BGV_E_ARG);
+  put_req* r = (put_req*)calloc(1, sizeof(put_req));
+  r->c = ctx;
+  r->first = first;
+  r->keys = keys;
+  r->n = len / (size_t)fmt;
+  r->fmt = fmt;
+  if (napi_create_promise(env, &r->deferred, &promise) != napi_ok ||
+      napi_create_reference(env, argv[0], 1, &r->ctx_ref) != napi_ok ||
+      napi_create_reference(env, argv[2], 1, &r->keys_ref) != napi_ok ||
+      napi_create_string_utf8(env, "blsgpu.pubkeysPut", NAPI_AUTO_LENGTH, &name) != napi_ok ||
+      napi_create_async_work(env, NULL, name, put_execute, put_complete, r, &r->work) != napi_ok ||
+      napi_queue_async_work(env, r->work) != napi_ok) {
+    napi_throw_error(env, NULL, "blsgpu: N-API failure");
+    return NULL;
+  }
+  return promise;
 }
 
 static napi_value js_keygen(napi_env env, napi_callback_info info) {
@@ -607,6 +683,7 @@ static napi_value init_module(napi_env env, napi_value exports) {
       {"close", NULL, js_close, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"strerror", NULL, js_strerror, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"pubkeysPut", NULL, js_pubkeys_put, NULL, NULL, NULL, METHOD_ATTR, NULL},
+      {"pubkeysPutAsync", NULL, js_pubkeys_put_async, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"keygen", NULL, js_keygen, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"sign", NULL, js_sign, NULL, NULL, NULL, METHOD_ATTR, NULL},
       {"verify", NULL, js_verify, NULL, NULL, NULL, METHOD_ATTR, NULL},

@@ -43,6 +43,8 @@ export interface BlsGpuVerifierOpts {
   maxBufferedSigs?: number;
   maxBufferWaitMs?: number;
   blsVerifyAllMultiThread?: boolean;
+  /** called once per uploaded run that held undecodable keys (those indices stay unusable) */
+  onPubkeyError?: (e: Error, first: number, n: number) => void;
 }
 
 export interface BlsGpuVerifierModules {
@@ -59,7 +61,9 @@ export declare class BlsGpuVerifier implements IBlsVerifier {
   close(): Promise<void>;
   /** state-transition pubkey-added hook: (index, 48-byte pubkey, PublicKey?) */
   pubkeyAddedHook(): (index: number, pubkey: Uint8Array, pk?: object) => void;
-  flushPubkeys(): void;
+  /** uploads the queued keys off the event loop; verifySignatureSets awaits it */
+  flushPubkeys(): Promise<void>;
+  onPubkeyError: ((e: Error, first: number, n: number) => void) | null;
   isValidBlsAggregate(publicKeys: PubkeyRef[], message: Uint8Array, signature: Uint8Array): Promise<boolean>;
   aggregateSignatures(sigs: Uint8Array[]): Uint8Array;
   aggregateSignaturesMany(aggregates: Uint8Array[][]): Uint8Array[];

@@ -193,6 +193,13 @@ int hs_hash_to_g2(uint8_t* out_aff, uint8_t* out_comp96, const uint8_t* msg, uin
 
 // P (test layout g1) , Q (test layout g2) -> Miller loop value and pairing^3
 void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12(out, miller_loop(in_g1(p), in_g2(q))); }
+// The bulk verify path's pairing value for one set: r P by the GLV randomizer (task_pk's
+// jac_mul_glv, P left Jacobian), H Jacobian, k_miller's miller_loop1, then final_exp (the
+// cube of the pairing) -- pinned against tests/golden/pairing.json
+void hs_bulk_pair_value(uint8_t* out, const uint8_t* p, const uint8_t* q, uint64_t word) {
+  const g1_jac rp = jac_mul_glv(jac_from_aff(in_g1(p)), word);
+  out_fp12(out, final_exp(miller_loop1(rp, jac_from_aff(in_g2(q)))));
+}
 void hs_final_exp(uint8_t* out, const uint8_t* f) { out_fp12(out, final_exp(in_fp12(f))); }
 // team-parallel closing arithmetic (bls_team.h), emulated lane by lane
 void hs_team_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {

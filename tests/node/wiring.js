@@ -57,6 +57,66 @@ const impls = {BlsSingleThreadVerifier: FakeSingle, BlsMultiThreadWorkerPool: Fa
     const bad = await v.verifySignatureSets([{type: "single", pubkey: 0, signingRoot: hex(s.msg).map((b, i) => (i ? b : b ^ 1)),
       signature: hex(s.sig)}]);
     assert.strictEqual(bad, false);
+
+    // a malformed key through the hook (advisor r03): its run is committed with the index
+    // marked, reported once, and neither blocks later keys nor verifies as a usable key
+    const reports = [];
+    v.onPubkeyError = (e, first, n) => reports.push([e.message, first, n]);
+    const junk = new Uint8Array(48);  // no compression flag: BLST_BAD_ENCODING
+    hook(1, junk, {});
+    await v.flushPubkeys();
+    assert.strictEqual(reports.length, 1, "one report for the bad run");
+    assert.match(reports[0][0], /BLST_BAD_ENCODING/);
+    hook(2, hex(gold.pk_compressed[2]), {});
+    const s2 = sigs.cases.find((x) => x.key === 2);
+    assert.strictEqual(await v.verifySignatureSets([{type: "single", pubkey: 2, signingRoot: hex(s2.msg),
+      signature: hex(s2.sig)}]), true, "a later key still uploads and verifies");
+    await assert.rejects(v.verifySignatureSets([{type: "single", pubkey: 1, signingRoot: hex(s.msg),
+      signature: hex(s.sig)}]), /index/i);
+    assert.strictEqual(reports.length, 1);
+
+    // 65,536 keys added through the hook while gossip-style calls run: the upload happens off
+    // the event loop (addon pubkeysPutAsync), so no event-loop gap exceeds one call's latency
+    const N = 65536;
+    const sks = new Uint8Array(32 * N);
+    for (let i = 0; i < N; i++) {
+      sks[32 * i + 31] = (i + 7) & 0xff;
+      sks[32 * i + 30] = ((i + 7) >> 8) & 0xff;
+      sks[32 * i + 29] = ((i + 7) >> 16) & 0xff;
+      sks[32 * i] = 0x11;
+    }
+    const {addon} = require(path.join(__dirname, "..", "..", "lodestar_amd", "node", "BlsGpuVerifier.js"));
+    const pks48 = addon.keygen(v.ctx, sks, -1);
+    const one = () => v.verifySignatureSets([{type: "single", pubkey: 0, signingRoot: hex(s.msg), signature: hex(s.sig)}],
+      {batchable: true});
+    const lat = [];
+    for (let k = 0; k < 20; k++) {
+      const t = process.hrtime.bigint();
+      assert.strictEqual(await one(), true);
+      lat.push(Number(process.hrtime.bigint() - t) / 1e6);
+    }
+    lat.sort((a, b) => a - b);
+    const callMs = lat[10];
+    let last = process.hrtime.bigint();
+    let maxGap = 0;
+    const ticker = setInterval(() => {
+      const t = process.hrtime.bigint();
+      maxGap = Math.max(maxGap, Number(t - last) / 1e6);
+      last = t;
+    }, 0);
+    const first = 3;
+    for (let i = 0; i < N; i++) hook(first + i, pks48.subarray(48 * i, 48 * i + 48), {});
+    const calls = [];
+    for (let k = 0; k < 64; k++) calls.push(one());
+    const res = await Promise.all(calls);
+    await v.flushPubkeys();
+    clearInterval(ticker);
+    assert.ok(res.every((x) => x === true));
+    const sN = await v.verifySignatureSets([{type: "single", pubkey: first + N - 1, signingRoot: hex(s.msg),
+      signature: hex(s.sig)}]);
+    assert.strictEqual(sN, false, "the last added key is in the cache (wrong signature for it: false)");
+    console.log(JSON.stringify({pubkey_upload: {keys: N, call_ms_p50: callMs, max_event_loop_gap_ms: maxGap}}));
+    assert.ok(maxGap <= Math.max(callMs, 5), `event loop stalled ${maxGap} ms (one call ${callMs} ms)`);
     await v.close();
   }
   console.log("wiring ok");

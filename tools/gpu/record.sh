@@ -1,0 +1,59 @@
+#!/bin/bash
+# One GPU-box session, parameterised (replaces the per-experiment session scripts of round 3).
+#   tools/gpu/record.sh OUTDIR STEP...
+# Steps, run in the order given; the first failing GPU step ends the session (no retries):
+#   suite    pytest -m gpu (thread timeouts, one process)
+#   smoke    __graft_entry__.smoke()
+#   bench    python bench.py (the default command the driver runs)  -> OUTDIR/bench_default.json
+#   quick    bench headline window only (no CPU baseline, no extras) -> OUTDIR/bench_quick.jsonl (appends)
+#   trace    rocprofv3 --kernel-trace --stats of the bench command   -> OUTDIR/bench_trace/
+#   roof     rocprofv3 --kernel-trace --stats of the isolated roofline call -> OUTDIR/roof_trace/
+#   pmc      the PMC passes of the roofline call (tools/gpu/pmc.sh)  -> gpurun_out/<basename OUTDIR>/pmc
+#   gossip   Node 64-caller gossip bench                             -> OUTDIR/gossip.jsonl
+#   ubench   the VALU / product microbenchmarks                      -> OUTDIR/ubench_*.jsonl
+set -o pipefail
+O=$1; shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+fail() { echo "step $1 failed (rc=$2)"; tail -20 "$3" 2>/dev/null; exit 1; }
+for step in "$@"; do
+  case $step in
+    suite)
+      timeout -k 10 500 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
+        > "$O/pytest_gpu.txt" 2>&1 || fail suite $? "$O/pytest_gpu.txt"
+      tail -1 "$O/pytest_gpu.txt" ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.txt" 2>&1 \
+        || fail smoke $? "$O/smoke.txt"
+      tail -1 "$O/smoke.txt" ;;
+    bench)
+      timeout -k 10 300 python bench.py > "$O/bench_default.json" 2> "$O/bench_default.err" \
+        || fail bench $? "$O/bench_default.err"
+      python tools/gpu/summarize.py "$O/bench_default.json" ;;
+    quick)
+      timeout -k 10 150 python bench.py --no-cpu-baseline --no-block-import --no-epoch-sweep \
+        >> "$O/bench_quick.jsonl" 2>> "$O/bench_quick.err" || fail quick $? "$O/bench_quick.err"
+      tail -1 "$O/bench_quick.jsonl" | python tools/gpu/summarize.py - ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/bench_trace" -o run --output-format csv \
+        -- python3 bench.py --no-cpu-baseline > "$O/bench_traced.json" 2> "$O/bench_traced.err" \
+        || fail trace $? "$O/bench_traced.err" ;;
+    roof)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/roof_trace" -o run --output-format csv \
+        -- python3 tools/gpu/roof_call.py > "$O/roof_call.json" 2> "$O/roof_call.err" \
+        || fail roof $? "$O/roof_call.err"
+      cat "$O/roof_call.json" ;;
+    pmc)
+      TAG=$(basename "$O") bash tools/gpu/pmc.sh || fail pmc $? /dev/null ;;
+    gossip)
+      timeout -k 10 200 node tests/node/gossip_bench.js 5 64 > "$O/gossip.jsonl" 2> "$O/gossip.err" \
+        || fail gossip $? "$O/gossip.err"
+      cat "$O/gossip.jsonl" ;;
+    ubench)
+      for u in ubench_valu ubench_fpmul; do
+        [ -x tools/$u ] || continue
+        timeout -k 10 120 tools/$u > "$O/$u.jsonl" 2>&1 || fail $u $? "$O/$u.jsonl"
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

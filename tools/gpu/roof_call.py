@@ -1,6 +1,6 @@
 """The bench's roofline measurement alone (bench.roofline_isolated): one 64,512-set verify
 call (k_miller = one wave per SIMD), repeated, on an idle device.  Driver for the PMC
-passes of tools/gpu/r02_pmc.sh."""
+passes of tools/gpu/pmc.sh and the `roof` step of tools/gpu/record.sh."""
 import json
 import os
 import sys
