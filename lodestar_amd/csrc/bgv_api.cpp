@@ -164,6 +164,8 @@ struct Exec {
   size_t pscratch_cap = 0;
   uint8_t* d_pout = nullptr;
   size_t pout_cap = 0;
+  uint32_t* d_lines = nullptr;  // the bulk Miller loop's line records (bgv_lines_pairs)
+  uint32_t lines_cap = 0;       // pairs
 };
 
 // bgv_final_verify's device buffers (under util_mu)
@@ -501,6 +503,23 @@ static int exec_reserve_groups(Exec& x, uint32_t groups) {
   return BGV_OK;
 }
 
+// line records for the batch's bulk Miller launch (none on the latency path): allocated on
+// first use, in steps of 16,384 pairs (368 MB), never shrunk
+static int exec_reserve_lines(Exec& x, bgv_dev_batch& b) {
+  const uint32_t need = bgv_lines_pairs(b);
+  if (need > x.lines_cap) {
+    const uint32_t cap = (need + 16383u) & ~16383u;
+    if (x.d_lines) (void)hipFree(x.d_lines);
+    x.d_lines = nullptr;
+    x.lines_cap = 0;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&x.d_lines), bgv_line_record_bytes() * cap));
+    x.lines_cap = cap;
+  }
+  b.lines = x.d_lines;
+  b.lines_cap = x.lines_cap;
+  return BGV_OK;
+}
+
 static int exec_create(Exec* x) {
   HIPCHK(hipEventCreate(&x->ev0));
   HIPCHK(hipEventCreate(&x->ev1));
@@ -512,7 +531,8 @@ static int exec_create(Exec* x) {
 
 static void exec_destroy(Exec* x) {
   if (x->main) (void)hipStreamSynchronize(x->main);
-  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx, x->d_pkb, x->d_pscratch, x->d_pout};
+  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx,
+                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   x->h_slots.release();
@@ -1076,6 +1096,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   b.max_npk = max_npk;
   b.uniq = x.d_idx + nidx;
   b.nuniq = (uint32_t)nuniq;
+  if (int lrc = exec_reserve_lines(x, b)) return lrc;
   bgv_streams S{x.main, prof ? x.kev : nullptr};
   int32_t *ss = x.h_ss.p, *ps = x.h_ps.p, *verdict = x.h_verdict.p;
   {
@@ -1780,8 +1801,9 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
     bgv_dev_batch b = make_batch(d, *x, nslots, ngroups);
     b.max_npk = max_npk;
     b.path = path;
+    rc = exec_reserve_lines(*x, b);
     bgv_streams S{x->main, nullptr};
-    const bool ok =
+    const bool ok = rc == BGV_OK &&
         hipMemcpyAsync(x->d_slots, slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x->main) ==
             hipSuccess &&
         hipMemcpyAsync(x->d_groups, groups.data(), sizeof(bgv_dgroup) * ngroups, hipMemcpyHostToDevice, x->main) ==

@@ -305,6 +305,16 @@ static uint32_t miller_round_lanes() {
   return lanes;
 }
 
+// BGV_MILLER_1PASS=1: the single-pass k_miller (one lane holds f, T and P) instead of
+// k_lines + k_facc, for A/B measurements; it needs no line records
+bool bgv_single_pass_miller() {
+  static const bool v = [] {
+    const char* e = getenv("BGV_MILLER_1PASS");
+    return e && atoi(e) > 0;
+  }();
+  return v;
+}
+
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   const uint32_t n = b.nslots;
   if (n == 0) return hipSuccess;
@@ -323,15 +333,20 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
     launch_miller_latency(b, n, b.ngroups, s.main);
   } else if (b.path != BGV_PATH_BULK && b.ngroups <= bgv_latency_max() &&
              (n + b.ngroups + R - 1) / R > (n + R - 1) / R) {
-    // the group pairs on extra k_miller lanes would open one more round of one wave per SIMD
+    // the group pairs on extra k_facc lanes would open one more round of one wave per SIMD
     // (131,072 sets + 2,048 groups: 3 rounds instead of 2); run them on teams instead
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, 0u,
                        b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
-    hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
-                       b.pk_status, b.f, 0u, b.gsum, b.gpair);
-  } else {
+    if (bgv_single_pass_miller())
+      hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
+                         b.pk_status, b.f, 0u, b.gsum, b.gpair);
+    else if (hipError_t e = bgv_launch_miller_bulk(b, 0u, s.main); e != hipSuccess)
+      return e;
+  } else if (bgv_single_pass_miller()) {
     hipLaunchKernelGGL(k_miller, dim3(nblk(n + b.ngroups, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h,
                        b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+  } else if (hipError_t e = bgv_launch_miller_bulk(b, b.ngroups, s.main); e != hipSuccess) {
+    return e;
   }
   BGV_MARK(3);
   return hipGetLastError();

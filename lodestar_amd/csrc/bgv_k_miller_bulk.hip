@@ -1,0 +1,128 @@
+// The bulk Miller loops of a verify call (gfx950), in two phases and in a unit of its own so
+// that each phase gets its own register budget (BGV_WPE_LINES / BGV_WPE_FACC waves per SIMD).
+// The per-set pairs of blst's randomized batch equation (maybeBatch.ts:18-25 ->
+// verifyMultipleAggregateSignatures):  f_i = MillerLoop(r_i pk_i, H(m_i)), and one pair per
+// device group g_g = MillerLoop(-G1, S_g).
+//
+//   k_lines  one lane per twist point Q (each distinct signing root's H, each group's S_g):
+//            walks T over the loop and writes the 68 P-free line records (bls_pairing.h
+//            lz_pline_dbl / lz_pline_add) to HBM.  Live set: T and one step's temporaries.
+//   k_facc   one lane per pair: f <- f^2 * line(P) over the records of its Q, the records
+//            staged through LDS one step ahead (global_load_lds, no VGPRs in flight).  Live
+//            set: f, P's three constants and the step's temporaries.
+//
+// One loop of the single-pass k_miller kept f (168 u32), T (84) and P (42) live across every
+// out-of-line product: 2.7 KB of scratch per lane and 230x its algorithmic HBM bytes
+// (DESIGN.md section 2).  Split, each phase's live set fits the registers the calling
+// convention preserves across a product call.
+//
+// Records: word d of record k (step k of the loop) of pair p is lines[(k * 84 + d) * cap + p]
+// (cap = the buffer's pairs): a wave's 64 lanes read and write 256 consecutive bytes.
+#include "bgv_device.h"
+
+#ifndef BGV_WPE_LINES
+#define BGV_WPE_LINES 1
+#endif
+#ifndef BGV_WPE_FACC
+#define BGV_WPE_FACC 1
+#endif
+#define BGV_KATTR_LINES __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_LINES, BGV_WPE_LINES)))
+#define BGV_KATTR_FACC __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BGV_WPE_FACC, BGV_WPE_FACC)))
+
+static_assert(sizeof(lz_pline_d) == 4 * BGV_LINE_WORDS, "line record layout");
+static_assert(sizeof(lz_pline_a) == 4 * BGV_LINE_WORDS, "line record layout");
+
+static __device__ const g1_jac kNegG1JacB = {{BGV_G1X}, {BGV_NEG_G1Y}, {BGV_ONE}};
+
+extern "C" {
+
+// Lanes [0, nq): the set pairs' twist points -- slot uniq[u] (b.uniq: the first slot of each
+// distinct signing root) or slot u; lanes [nq, nq + ngroups): group g's S_g at record index
+// nslots + g.  Padding slots (no H) and infinite S_g write nothing (k_facc outputs 1 there).
+__global__ void BGV_KATTR_LINES k_lines(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                        const g2_jac* __restrict__ h, const uint32_t* __restrict__ uniq,
+                                        uint32_t nq, uint32_t ngroups, const g2_jac* __restrict__ gsum,
+                                        uint32_t* __restrict__ lines, uint32_t cap) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t p;
+  const g2_jac* q;
+  if (u < nq) {
+    p = uniq ? uniq[u] : u;
+    if (slots[p].flags & BGV_SLOT_PAD) return;
+    q = h + p;
+  } else if (u - nq < ngroups) {
+    p = nslots + (u - nq);
+    q = gsum + (u - nq);
+    if (jac_is_inf(*q)) return;
+  } else {
+    return;
+  }
+  uint32_t* base = lines + p;
+  miller_lines_walk(q, [&](int k, const auto& rec) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&rec);
+    uint32_t* dst = base + (size_t)k * BGV_LINE_WORDS * cap;
+    BGV_UNROLL for (int d = 0; d < BGV_LINE_WORDS; ++d) dst[(size_t)d * cap] = w[d];
+  });
+}
+
+// Lanes [0, nslots): f_i over the records of the slot's signing root (slots[s].hsrc), 1 for a
+// slot that takes no part; lanes [nslots, nslots + ngroups): g_g = MillerLoop(-G1, S_g) (1 for
+// an infinite S_g).
+__global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint32_t nslots,
+                                      const g1_jac* __restrict__ rpk, const int32_t* __restrict__ sig_status,
+                                      const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ lines,
+                                      uint32_t cap, fp12_t* __restrict__ f, uint32_t ngroups,
+                                      const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  bool live;
+  uint32_t lp;
+  const g1_jac* P;
+  fp12_t* out;
+  if (s < nslots) {
+    live = slot_live(slots[s], sig_status[s], pk_status[s]);
+    lp = slots[s].hsrc;
+    P = rpk + s;
+    out = f + s;
+  } else if (s - nslots < ngroups) {
+    const uint32_t g = s - nslots;
+    live = !jac_is_inf(gsum[g]);
+    lp = nslots + g;
+    P = &kNegG1JacB;
+    out = gpair + g;
+  } else {
+    return;
+  }
+  if (!live) {
+    *out = fp12_one();
+    return;
+  }
+  const uint32_t* base = lines + lp;
+  *out = miller_facc_walk(*P, [&](int k, auto* rec) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(rec);
+    const uint32_t* src = base + (size_t)k * BGV_LINE_WORDS * cap;
+    BGV_UNROLL for (int d = 0; d < BGV_LINE_WORDS; ++d) w[d] = src[(size_t)d * cap];
+  });
+}
+
+}  // extern "C"
+
+// line records a batch's bulk Miller launch writes: one per set pair's twist point (slot index
+// space) and one per group; 0 when the batch takes the latency path or has no slots
+uint32_t bgv_lines_pairs(const bgv_dev_batch& b) {
+  if (b.nslots == 0 || bgv_use_latency(b, b.nslots + b.ngroups) || bgv_single_pass_miller()) return 0;
+  return b.nslots + b.ngroups;
+}
+size_t bgv_line_record_bytes() { return (size_t)BGV_MILLER_STEPS * BGV_LINE_WORDS * 4; }
+
+// the set pairs [0, nslots) and the group pairs [nslots, nslots + ngroups) of a bulk batch;
+// ngroups = 0 when the group pairs run on teams instead (bgv_launch_miller)
+hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipStream_t st) {
+  if (!b.lines || b.lines_cap < b.nslots + ngroups) return hipErrorInvalidValue;
+  const uint32_t nq = b.uniq ? b.nuniq : b.nslots;
+  if (nq + ngroups)
+    hipLaunchKernelGGL(k_lines, dim3(nblk(nq + ngroups, 64)), dim3(64), 0, st, b.slots, b.nslots, b.h, b.uniq, nq,
+                       ngroups, b.gsum, b.lines, b.lines_cap);
+  hipLaunchKernelGGL(k_facc, dim3(nblk(b.nslots + ngroups, 64)), dim3(64), 0, st, b.slots, b.nslots, b.rpk,
+                     b.sig_status, b.pk_status, b.lines, b.lines_cap, b.f, ngroups, b.gsum, b.gpair);
+  return hipGetLastError();
+}

@@ -55,6 +55,10 @@ struct bgv_dev_batch {
   // bgv_dgroup.ref1 - 1; null otherwise
   const fp12_t* gu1;
   int32_t* verdict;    // per group: bit 0 = the group passes, bit 1 = its pairing value equals ref's
+  // the bulk Miller loop's line records (bgv_k_miller_bulk.hip): lines_cap pairs, SoA; null
+  // unless the host reserved them (bgv_lines_pairs)
+  uint32_t* lines;
+  uint32_t lines_cap;
 #ifdef BGV_KERNEL_SIDE
   const aff_t<fp_t>* cache_ptr() const { return reinterpret_cast<const aff_t<fp_t>*>(cache_opaque); }
 #endif
@@ -77,6 +81,11 @@ bool bgv_sig_pairs(const bgv_dev_batch& b);
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree);  // bgv_k_prep_bulk.hip
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
+// bulk path: k_lines + k_facc over the set pairs and the first ngroups group pairs
+hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipStream_t st);
+uint32_t bgv_lines_pairs(const bgv_dev_batch& b);  // line records the batch needs (0: latency path)
+bool bgv_single_pass_miller();                     // BGV_MILLER_1PASS: k_miller instead (A/B)
+size_t bgv_line_record_bytes();                    // bytes of one pair's 68 records
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
 size_t bgv_slot_bytes();

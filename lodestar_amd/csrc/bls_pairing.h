@@ -3,6 +3,8 @@
 // exponentiation (easy part + x-chain hard part computing the cube of the
 // pairing, which has the same kernel since gcd(3, r) = 1).
 #pragma once
+#include <type_traits>
+
 #include "bls_curve.h"
 #include "bls_lazy.h"
 
@@ -254,6 +256,166 @@ BGV_MILLER_LOOP_ATTR fp12_t miller_loop1m(const g1_jac* pm, const g2_jac* qm) {
   return fp12_conj(lz12_out(f));
 }
 BGV_HD fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) { return miller_loop1m(&p, &q); }
+
+// ---------------------------------------------------------------------------
+// The same Miller loop split in two phases (the bulk verify path: k_lines, k_facc).
+//   k_lines  walks the twist point T over the loop and emits each step's line WITHOUT the G1
+//            factors (they are the only place P enters):  l0 = L0 Z_P^3,  l1 = L1 (-X_P Z_P),
+//            l3 = L3 Y_P, with (L0, L1, L3) below.  Lines depend on Q only, so a signing root
+//            shared by many sets is walked once (hash_to_G2 once per root, bgv_dslot.hsrc).
+//   k_facc   keeps only f and P: per step f <- f^2 * (L scaled by P).
+// The scaled lines are the same field elements as lz_miller_dbl_lines / miller_add_jq's, so
+// f is the same field element as miller_loop1m's (bit-identical after canonicalisation).
+// Line record: 68 steps (the first doubling, then per bit 61..0 an addition where the next
+// bit of |x| is set and a doubling) x (L0, L1, L3) = 6 Fp = 84 u32 limbs.
+// ---------------------------------------------------------------------------
+#define BGV_MILLER_STEPS 68
+#define BGV_LINE_WORDS (6 * NL)
+
+template <class A, class B, class C>
+struct lz_pline_t {
+  A L0;
+  B L1;
+  C L3;
+};
+
+// doubling step: L0 = 3 X^3 - 2 Y^2, L1 = 3 X^2 Z^2, L3 = Z3 Z^2 (E = 3A as in lz_miller_dbl_lines)
+BGV_MILLER_ATTR auto lz_pline_dbl(lz_tpt& t) {
+  const lz2r A = lz2_sqr(t.x);
+  const lz2r B = lz2_sqr(t.y);
+  const lz2r C = lz2_sqr(B);
+  const lz2r ZZ = lz2_sqr(t.z);
+  const auto D = lz2_norm(lz2_dbl(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.x, B))), lz2_add(A, C))));
+  const auto L0 = lz2_norm(lz2_sub(lz2_mulk<3>(lz2_mul(A, t.x)), lz2_dbl(B)));
+  const auto L1 = lz2_norm(lz2_mulk<3>(lz2_mul(A, ZZ)));
+  const auto X3 = lz2_sub(lz2_mulk<9>(lz2_sqr(A)), lz2_dbl(D));
+  const auto Y3 = lz2_sub(lz2_mulk<3>(lz2_mul(A, lz2_norm(lz2_sub(D, X3)))), lz2_mulk<8>(C));
+  const auto Z3 = lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.y, t.z))), lz2_add(B, ZZ));
+  const auto L3 = lz2_norm(lz2_mul(Z3, ZZ));
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+  return lz_pline_t<std::decay_t<decltype(L0)>, std::decay_t<decltype(L1)>, std::decay_t<decltype(L3)>>{L0, L1, L3};
+}
+
+// addition step T + Q, Q = (X2 : Y2 : Z2) Jacobian (miller_add_jq without the P factors):
+// L0 = r X2 Z2 - Y2 Z3, L1 = r Z2^3, L3 = Z3 Z2^3
+BGV_MILLER_ATTR auto lz_pline_add(lz_tpt& t, const lz2r& qx, const lz2r& qy, const lz2r& qz) {
+  const lz2r zz = lz2_sqr(qz);
+  const auto zzz = lz2_norm(lz2_mul(zz, qz));
+  const auto xz = lz2_norm(lz2_mul(qx, qz));
+  const lz2r ZZ = lz2_sqr(t.z);
+  const auto U1 = lz2_mul(t.x, zz);
+  const auto U2 = lz2_mul(qx, ZZ);
+  const auto S1 = lz2_mul(t.y, zzz);
+  const auto S2 = lz2_mul(qy, lz2_mul(t.z, ZZ));
+  const auto H = lz2_norm(lz2_sub(U2, U1));
+  const lz2r HH = lz2_sqr(H);
+  const auto J = lz2_mulk<4>(lz2_mul(H, HH));
+  const lz2r r = lz2_red(lz2_dbl(lz2_sub(S2, S1)));
+  const auto V = lz2_mulk<4>(lz2_mul(U1, HH));
+  const auto X3 = lz2_norm(lz2_sub(lz2_sqr(r), lz2_add(J, lz2_dbl(V))));
+  const auto Y3 = lz2_sub(lz2_mul(r, lz2_norm(lz2_sub(V, X3))), lz2_dbl(lz2_mul(S1, lz2_norm(J))));
+  const auto Z3 = lz2_mul(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, qz))), lz2_add(ZZ, zz)), H);
+  const auto L0 = lz2_norm(lz2_sub(lz2_mul(r, xz), lz2_mul(qy, Z3)));
+  const auto L1 = lz2_norm(lz2_mul(r, zzz));
+  const auto L3 = lz2_norm(lz2_mul(Z3, zzz));
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+  return lz_pline_t<std::decay_t<decltype(L0)>, std::decay_t<decltype(L1)>, std::decay_t<decltype(L3)>>{L0, L1, L3};
+}
+
+// the record types the two phases agree on
+typedef decltype(lz_pline_dbl(*(lz_tpt*)nullptr)) lz_pline_d;
+typedef decltype(lz_pline_add(*(lz_tpt*)nullptr, lz2r{}, lz2r{}, lz2r{})) lz_pline_a;
+
+// the line of a record scaled by P (6 products), as an Fp12 factor's three coefficients
+template <class Lp>
+BGV_HD void lz_pline_scale(const Lp& L, const lz_mp& P, lz2r* l0, lz2r* l1, lz2r* l3) {
+  *l0 = lz2_mul_fp(L.L0, P.zp3);
+  *l1 = lz2_mul_fp(L.L1, P.xn);
+  *l3 = lz2_mul_fp(L.L3, P.yp);
+}
+
+// k_facc's steps: the first doubling (f = its line), an addition (f * line), a doubling (f^2 * line)
+template <class Lp>
+BGV_HD lzf12 lz_facc_first(const Lp& L, const lz_mp& P) {
+  lz2r l0, l1, l3;
+  lz_pline_scale(L, P, &l0, &l1, &l3);
+  const lz2r z = lz2r{lz_in(fp_zero()), lz_in(fp_zero())};
+  return lzf12{lz6<LMASK, 2>{l0, l1, z}, lz6<LMASK, 2>{z, l3, z}};
+}
+template <class Lp>
+BGV_HD lzf12 lz_facc_add(const lzf12& f, const Lp& L, const lz_mp& P) {
+  lz2r l0, l1, l3;
+  lz_pline_scale(L, P, &l0, &l1, &l3);
+  return lz12_red(lz12_mul_line(f, l0, l1, l3));
+}
+// A word that is always 0 but depends on every coefficient of f: an index built from it keeps
+// the compiler from issuing a step's record loads before f^2 exists (hoisted, the 84 loaded
+// words stay live across the whole squaring and push f's temporaries into scratch).
+BGV_HD uint32_t lz12_after(const lzf12& f) {
+  uint32_t z = 0;
+  const lz2r* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+  BGV_UNROLL for (int i = 0; i < 6; ++i) z ^= c[i]->c0.v[0] ^ c[i]->c1.v[0];
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(z));
+#else
+  asm volatile("" : "+r"(z));
+  z = 0;
+#endif
+  return z;
+}
+template <class Load>
+BGV_HD lzf12 lz_facc_dbl_load(const lzf12& f, int k, Load load, const lz_mp& P) {
+  const lzf12 f2 = lz12_red(lz12_sqr(f));
+  lz_pline_d L;
+  load(k + (int)lz12_after(f2), &L);
+  lz2r l0, l1, l3;
+  lz_pline_scale(L, P, &l0, &l1, &l3);
+  return lz12_red(lz12_mul_line(f2, l0, l1, l3));
+}
+
+// bit i + 1 of |x| is set: an addition step precedes doubling step i (i = 61..0)
+BGV_HD bool miller_add_at(int i) { return (BGV_X_ABS >> (i + 1)) & 1; }
+
+// The line records of one twist point in loop order (k_lines' walk; also the host reference).
+// Q is read from memory at the 5 additions (an opaque index keeps the compiler from hoisting
+// the loads), so the 63 doublings keep only T and their temporaries live.
+template <class Emit>
+BGV_HD void miller_lines_walk(const g2_jac* qm, Emit emit) {
+  lz_tpt t = {lz2_in(qm[0].x), lz2_in(qm[0].y), lz2_in(qm[0].z)};
+  int k = 0;
+  emit(k++, lz_pline_dbl(t));
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (miller_add_at(i)) {
+      const g2_jac& q = qm[bgv_opaque0()];
+      emit(k++, lz_pline_add(t, lz2_in(q.x), lz2_in(q.y), lz2_in(q.z)));
+    }
+    emit(k++, lz_pline_dbl(t));
+  }
+}
+
+// k_facc's walk over one pair's records (load(k, rec) fills record k); returns f, conjugated
+template <class Load>
+BGV_HD fp12_t miller_facc_walk(const g1_jac& p, Load load) {
+  const miller_p P0 = miller_p_make(p);
+  const lz_mp P = {lz_in(P0.xn), lz_in(P0.yp), lz_in(P0.zp3)};
+  int k = 0;
+  lz_pline_d d;
+  load(k++, &d);
+  lzf12 f = lz_facc_first(d, P);
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (miller_add_at(i)) {
+      lz_pline_a a;
+      load(k++, &a);
+      f = lz_facc_add(f, a, P);
+    }
+    f = lz_facc_dbl_load(f, k++, load, P);
+  }
+  return fp12_conj(lz12_out(f));
+}
 
 // a^|x| in the cyclotomic subgroup, conjugated: a^x (x < 0)
 BGV_NOINLINE fp12_t cyclotomic_pow_x(const fp12_t& a) {

@@ -193,6 +193,33 @@ int hs_hash_to_g2(uint8_t* out_aff, uint8_t* out_comp96, const uint8_t* msg, uin
 
 // P (test layout g1) , Q (test layout g2) -> Miller loop value and pairing^3
 void hs_miller_loop(uint8_t* out, const uint8_t* p, const uint8_t* q) { out_fp12(out, miller_loop(in_g1(p), in_g2(q))); }
+// The bulk path's two-phase Miller loop (k_lines' records, then k_facc's walk) on one pair,
+// P and Q Jacobian from affine inputs scaled by z1 / z2 (1: affine)
+void hs_miller_two_phase(uint8_t* out, const uint8_t* p, const uint8_t* q, const uint8_t* z1, const uint8_t* z2) {
+  const g1_aff pa = in_g1(p);
+  const g2_aff qa = in_g2(q);
+  const fp_t zp = in_fp(z1);
+  const fp2_t zq = in_fp2(z2);
+  const fp_t zp2 = fp_sqr(zp);
+  const fp2_t zq2 = fp2_sqr(zq);
+  const g1_jac P = {fp_mul(pa.x, zp2), fp_mul(pa.y, fp_mul(zp2, zp)), zp};
+  const g2_jac Q = {fp2_mul(qa.x, zq2), fp2_mul(qa.y, fp2_mul(zq2, zq)), zq};
+  static uint32_t rec[BGV_MILLER_STEPS][BGV_LINE_WORDS];
+  miller_lines_walk(&Q, [&](int k, const auto& r) { memcpy(rec[k], &r, sizeof(r)); });
+  out_fp12(out, miller_facc_walk(P, [&](int k, auto* r) { memcpy(r, rec[k], sizeof(*r)); }));
+}
+// the single-pass loop on the same Jacobian inputs
+void hs_miller_one_pass(uint8_t* out, const uint8_t* p, const uint8_t* q, const uint8_t* z1, const uint8_t* z2) {
+  const g1_aff pa = in_g1(p);
+  const g2_aff qa = in_g2(q);
+  const fp_t zp = in_fp(z1);
+  const fp2_t zq = in_fp2(z2);
+  const fp_t zp2 = fp_sqr(zp);
+  const fp2_t zq2 = fp2_sqr(zq);
+  const g1_jac P = {fp_mul(pa.x, zp2), fp_mul(pa.y, fp_mul(zp2, zp)), zp};
+  const g2_jac Q = {fp2_mul(qa.x, zq2), fp2_mul(qa.y, fp2_mul(zq2, zq)), zq};
+  out_fp12(out, miller_loop1(P, Q));
+}
 // The bulk verify path's pairing value for one set: r P by the GLV randomizer (task_pk's
 // jac_mul_glv, P left Jacobian), H Jacobian, k_miller's miller_loop1, then final_exp (the
 // cube of the pairing) -- pinned against tests/golden/pairing.json

@@ -47,9 +47,7 @@ def test_pubkeys_put_marks_undecodable_and_appends():
         assert codes == [1, 1]
         s5 = next(x for x in sig_cases if x["key"] == 5)
         bad = ([native.SetSpec(bytes.fromhex(s5["msg"]), bytes.fromhex(s5["sig"]), pk_indices=[5])], True)
-        with pytest.raises(native.BlsGpuError) as e:
-            c.verify_jobs([bad], native.MODE_WORKER)
-        assert e.value.code == native.BGV_E_BAD_INDEX
+        assert c.verify_jobs([bad], native.MODE_WORKER) == [-native.BGV_E_BAD_INDEX]
         # overwriting the marked index with the real key clears the mark
         c.pubkeys_put(5, keys[5])
         assert c.verify_jobs([bad], native.MODE_WORKER) == [1]
@@ -65,6 +63,7 @@ def test_pubkeys_append_while_verifying():
     sig_cases = load("signatures.json")["cases"]
     c = native.Context()
     try:
+        keys = keys[:128]
         c.pubkeys_put(0, b"".join(keys))
         s = next(x for x in sig_cases if x["key"] == 3)
         job = ([native.SetSpec(bytes.fromhex(s["msg"]), bytes.fromhex(s["sig"]), pk_indices=[3])], True)
@@ -80,7 +79,7 @@ def test_pubkeys_append_while_verifying():
         th = threading.Thread(target=verifier)
         th.start()
         n0 = len(keys)
-        block = b"".join(keys) * 64  # 8192 keys per put (repeated valid keys)
+        block = b"".join(keys) * 64  # 8192 keys per put (the 128 keys repeated)
         for k in range(8):
             c.pubkeys_put(n0 + 8192 * k, block)
         stop.set()

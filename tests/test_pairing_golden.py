@@ -61,3 +61,23 @@ def test_bulk_kernel_math_matches_golden():
         L.hs_bulk_pair_value(out, hs.g1_b(pk), hs.g2_b(h), ctypes.c_uint64(int(s["word"], 16)))
         gt = f12_from_bytes(bytes.fromhex(s["gt"]))
         assert f12_from_bytes(out.raw) == o.f12_mul(o.f12_sqr(gt), gt)
+
+
+def test_two_phase_miller_equals_single_pass():
+    """k_lines + k_facc (P-free line records, then f over the records scaled by P) give the
+    same field element f as the single-pass miller_loop1m, for Jacobian P and Q with random Z
+    (the bulk path's inputs are Jacobian); bit-identical after canonicalisation."""
+    import ctypes
+    import random
+    L = hs.lib()
+    rng = random.Random(4)
+    for _ in range(3):
+        pk = o.g1_mul(o.G1, rng.randrange(1, o.R))
+        h = o.hash_to_g2(rng.randbytes(32))
+        z1 = hs.fp_b(rng.randrange(1, o.P))
+        z2 = hs.fp2_b((rng.randrange(o.P), rng.randrange(o.P)))
+        a, b = hs.buf(576), hs.buf(576)
+        L.hs_miller_two_phase(a, hs.g1_b(pk), hs.g2_b(h), z1, z2)
+        L.hs_miller_one_pass(b, hs.g1_b(pk), hs.g2_b(h), z1, z2)
+        assert a.raw == b.raw
+        assert o.final_exp(f12_from_bytes(a.raw)) == o.pairing(pk, h) if _ == 0 else True

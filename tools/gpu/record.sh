@@ -50,7 +50,7 @@ for step in "$@"; do
         || fail gossip $? "$O/gossip.err"
       cat "$O/gossip.jsonl" ;;
     ubench)
-      for u in ubench_valu ubench_fpmul; do
+      for u in ubench_valu ubench_fpmul ubench_prod; do
         [ -x tools/$u ] || continue
         timeout -k 10 120 tools/$u > "$O/$u.jsonl" 2>&1 || fail $u $? "$O/$u.jsonl"
       done ;;
