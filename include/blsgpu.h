@@ -163,6 +163,13 @@ int bgv_hash_to_g2(bgv_ctx* ctx, const uint8_t* msgs, const uint32_t* lens, size
  * first pubkey code (1 = infinity aggregate: BLST_PK_IS_INFINITY for >= 2 sets, false for
  * one), else the verdict (lodestar_amd/shard.py). */
 int bgv_verify_partial(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, uint8_t out576[576], int32_t out_codes[2]);
+/* One process over several devices: a context created on a device list spreads every
+ * bgv_verify / bgv_verify_async call of at least min_sets sets over its devices -- a job of
+ * at least min_sets sets as one run of sets per device whose Fp12 partials are combined with
+ * one final exponentiation, the other jobs in contiguous runs pinned to one device each
+ * (chain/bls/multithread/index.ts:153-166 splits big calls over workers the same way).
+ * Codes are those of the unsplit call.  Default 4096 (BGV_SPLIT_MIN env); 0 disables. */
+int bgv_set_split(bgv_ctx* ctx, uint32_t min_sets);
 int bgv_final_verify(bgv_ctx* ctx, const uint8_t* partials, size_t n, int32_t* out_verdict);
 
 /* Parity hook (tests only): the per-set intermediates of a verify call's kernels with the

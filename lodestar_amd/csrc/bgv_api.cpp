@@ -90,6 +90,14 @@ static size_t idle_coalesce_us() {
   static const size_t v = env_size("BGV_IDLE_COALESCE_US", BGV_IDLE_COALESCE_US, 0);
   return v;
 }
+// calls of at least this many sets on a context with several devices are spread over them
+// (verify_split; BGV_SPLIT_MIN env, bgv_set_split; 0 disables): a range-sync call ("64 blocks
+// ~ 8000 signatures", chain/bls/multithread/index.ts:34) takes every device
+#define BGV_SPLIT_MIN_SETS 4096
+static size_t split_min_env() {
+  static const size_t v = env_size("BGV_SPLIT_MIN", BGV_SPLIT_MIN_SETS, 0);
+  return v;
+}
 static int dispatchers_per_device() {
   static const int v = (int)env_size("BGV_DISPATCHERS", BGV_DISPATCHERS, 1);
   return v;
@@ -381,6 +389,7 @@ struct Call {
   // bgv_verify_partial: the call's Miller-loop product (576 B) and its two status codes
   uint8_t* partial_out = nullptr;
   int32_t* partial_codes = nullptr;
+  int dev = -1;  // index in bgv_ctx::devs of the only device whose dispatchers may take it (-1: any)
   bgv_job pjob{};
   int32_t pcode = 0;
   uint32_t slot_base = 0;  // offset of this call's slots in the merged batch
@@ -420,6 +429,11 @@ struct bgv_ctx {
   std::atomic<uint32_t> coalesce{BGV_COALESCE_US};
   std::atomic<uint32_t> idle_coalesce{BGV_IDLE_COALESCE_US};
   std::atomic<int> running{0};  // super-batches being run by dispatchers
+  // calls of at least this many sets are spread over the devices (verify_split; 0: never)
+  std::atomic<uint32_t> split_min{BGV_SPLIT_MIN_SETS};
+  std::atomic<int> split_inflight{0};  // asynchronous split calls not yet done (bgv_close waits)
+  std::mutex split_mu;
+  std::condition_variable split_cv;
   double kernel_ms[BGV_NKERNELS] = {};
   uint64_t kernel_launches = 0;
   // dispatch
@@ -626,8 +640,9 @@ static void call_fail(Call* call, int rc) {
 
 // host-side checks and layout, on the caller's thread
 static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets,
-                       int mode, int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user) {
+                       int mode, int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user, int dev = -1) {
   call->t0 = std::chrono::steady_clock::now();
+  call->dev = dev;
   if (c->closed) return -BGV_E_CLOSED;
   if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
   if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
@@ -698,7 +713,10 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
     if (c->stop) return -BGV_E_CLOSED;
     c->queue.push_back(call);
   }
-  c->qcv.notify_one();
+  if (dev < 0)
+    c->qcv.notify_one();
+  else
+    c->qcv.notify_all();  // only the pinned device's dispatchers may take it
   return BGV_OK;
 }
 
@@ -1316,18 +1334,27 @@ static void retry_loop(bgv_ctx* c, Device* d) {
 
 static void dispatcher_loop(bgv_ctx* c, Device* d, hipStream_t stream) {
   (void)hipSetDevice(d->id);
+  const int di = (int)(d - c->devs.data());
+  // a call pinned to another device (a shard of a split call, verify_split) is not ours
+  auto mine = [di](const Call* q) { return q->dev < 0 || q->dev == di; };
+  auto any_mine = [c, &mine] {
+    for (Call* q : c->queue)
+      if (mine(q)) return true;
+    return false;
+  };
   for (;;) {
     std::vector<Call*> calls;
     {
       std::unique_lock<std::mutex> lk(c->qmu);
-      c->qcv.wait(lk, [c] { return c->stop || !c->queue.empty(); });
-      if (c->queue.empty()) return;
+      c->qcv.wait(lk, [c, &any_mine] { return c->stop || any_mine(); });
+      if (!any_mine()) return;  // stopping, and nothing of ours left to drain
       // Coalescing window: a super-batch costs about the same device time from a
       // few thousand to ~10^5 sets (its closing phases are latency-bound), so give
       // concurrent callers a moment to join before launching.
-      auto queued_slots = [c] {
+      auto queued_slots = [c, &mine] {
         size_t n = 0;
-        for (Call* q : c->queue) n += q->L.slots.size();
+        for (Call* q : c->queue)
+          if (mine(q)) n += q->L.slots.size();
         return n;
       };
       const size_t cap = c->max_slots.load();
@@ -1338,17 +1365,21 @@ static void dispatcher_loop(bgv_ctx* c, Device* d, hipStream_t stream) {
       while (!c->stop && queued_slots() < cap &&
              c->qcv.wait_until(lk, until) != std::cv_status::timeout) {
       }
-      if (c->queue.empty()) continue;
+      if (!any_mine()) continue;
       size_t slots = 0;
-      while (!c->queue.empty()) {
-        Call* call = c->queue.front();
+      for (auto it = c->queue.begin(); it != c->queue.end();) {
+        Call* call = *it;
+        if (!mine(call)) {
+          ++it;
+          continue;
+        }
         const size_t n = call->L.slots.size();
         if (!calls.empty() && slots + n > cap) break;
         calls.push_back(call);
         slots += n;
-        c->queue.pop_front();
+        it = c->queue.erase(it);
       }
-      if (!c->queue.empty()) c->qcv.notify_one();
+      if (!c->queue.empty()) c->qcv.notify_all();
     }
     Exec* x = exec_acquire(*d);
     x->main = stream;
@@ -1418,6 +1449,7 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   c->max_slots = (uint32_t)max_batch_slots();
   c->coalesce = (uint32_t)coalesce_us();
   c->idle_coalesce = (uint32_t)idle_coalesce_us();
+  c->split_min = (uint32_t)split_min_env();
   const int n = (devices && ndev > 0) ? ndev : 1;
   c->devs.resize(n);
   for (int i = 0; i < n; ++i) {
@@ -1456,6 +1488,11 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
 
 int bgv_close(bgv_ctx* c) {
   if (!c) return -BGV_E_ARG;
+  {
+    // asynchronous split calls finish first: their pieces need the dispatchers
+    std::unique_lock<std::mutex> lk(c->split_mu);
+    c->split_cv.wait(lk, [c] { return c->split_inflight.load() == 0; });
+  }
   {
     std::lock_guard<std::mutex> lk(c->qmu);
     c->stop = true;
@@ -1641,9 +1678,173 @@ int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, i
   return first_err ? -first_err : BGV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// One call over several devices (a context on a device list; SURVEY 8(e) inside the library).
+// The reference splits a big call into >= 128-set jobs for its workers
+// (chain/bls/multithread/index.ts:153-166; range sync hands ~8000 sets at once, :34); here a
+// call of at least split_min sets is spread over the context's devices:
+//   * a job of at least split_min sets is cut into one contiguous run of sets per device; each
+//     run's Miller-loop product (576 B, bgv_verify_partial's) is computed on its device, the
+//     partials are combined with ONE final exponentiation (bgv_final_verify on the first
+//     device), and the job's code follows the reference's precedence: the first undecodable
+//     signature in set order, then the pubkey condition, then the verdict;
+//   * the other jobs go to the devices in contiguous runs balanced by set count, each run one
+//     call pinned to its device (retry rounds stay on the device that ran the first pass).
+// Codes are those of the same call on one device (tests/test_gpu_r04.py).
+// ---------------------------------------------------------------------------
+static int partial_submit(bgv_ctx* c, Call* call, const bgv_set* sets, size_t nsets, uint8_t* out576,
+                          int32_t* out_codes, int dev);
+static int call_wait(Call* call);
+static int partial_finish(Call* call, int rc, int32_t* out_codes);
+
+static size_t split_min_sets(const bgv_ctx* c) {
+  return c->split_min.load();
+}
+
+static void stats_add(bgv_stats* a, const bgv_stats& b) {
+  a->batch_retries += b.batch_retries;
+  a->batch_sigs_success += b.batch_sigs_success;
+  a->device_groups += b.device_groups;
+  a->sets_verified += b.sets_verified;
+  a->device_ms = std::max(a->device_ms, b.device_ms);
+}
+
+static bool split_wanted(const bgv_ctx* c, size_t nsets) {
+  return c->devs.size() > 1 && split_min_sets(c) > 0 && nsets >= split_min_sets(c);
+}
+
+static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
+                        int32_t* out, bgv_stats* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t K = c->devs.size(), big = split_min_sets(c);
+  struct Shard {  // one run of a big job on one device
+    Call call;
+    size_t job;
+    uint8_t part[576];
+    int32_t codes[2] = {0, 0};
+    int rc = BGV_OK;
+  };
+  struct Child {  // small jobs [j0, j1) pinned to one device
+    Call call;
+    std::vector<bgv_job> jobs;
+    std::vector<int32_t> out;
+    bgv_stats st{};
+    size_t j0 = 0;
+    int rc = BGV_OK;
+  };
+  std::vector<std::unique_ptr<Shard>> shards;
+  std::vector<std::unique_ptr<Child>> kids;
+  std::vector<size_t> small;
+  size_t small_sets = 0;
+  for (size_t j = 0; j < njobs; ++j) {
+    if ((size_t)jobs[j].first_set + jobs[j].n_sets > nsets) return -BGV_E_ARG;
+    if (jobs[j].n_sets >= big) continue;
+    small.push_back(j);
+    small_sets += jobs[j].n_sets;
+  }
+  int rc = BGV_OK;
+  // small jobs: contiguous runs of the call's job order, about small_sets / K sets each
+  {
+    size_t i = 0, acc = 0;
+    for (size_t d = 0; d < K && i < small.size(); ++d) {
+      const size_t target = (small_sets * (d + 1) + K - 1) / K;
+      auto kid = std::make_unique<Child>();
+      kid->j0 = i;
+      while (i < small.size() && (acc < target || kid->jobs.empty())) {
+        kid->jobs.push_back(jobs[small[i]]);
+        acc += jobs[small[i]].n_sets;
+        ++i;
+      }
+      if (d == K - 1)
+        while (i < small.size()) {
+          kid->jobs.push_back(jobs[small[i]]);
+          ++i;
+        }
+      kid->out.assign(kid->jobs.size(), 0);
+      kid->rc = call_submit(c, &kid->call, kid->jobs.data(), kid->jobs.size(), sets, nsets, mode, kid->out.data(),
+                            &kid->st, nullptr, nullptr, (int)d);
+      if (kid->rc != BGV_OK && rc == BGV_OK) rc = kid->rc;
+      kids.push_back(std::move(kid));
+    }
+  }
+  // big jobs: one run of sets per device
+  for (size_t j = 0; j < njobs; ++j) {
+    const uint32_t n = jobs[j].n_sets;
+    if (n < big) continue;
+    for (size_t d = 0; d < K; ++d) {
+      const size_t lo = n * d / K, hi = n * (d + 1) / K;
+      if (hi <= lo) continue;
+      auto sh = std::make_unique<Shard>();
+      sh->job = j;
+      sh->rc = partial_submit(c, &sh->call, sets + jobs[j].first_set + lo, hi - lo, sh->part, sh->codes, (int)d);
+      if (sh->rc != BGV_OK && rc == BGV_OK) rc = sh->rc;
+      shards.push_back(std::move(sh));
+    }
+  }
+  // every submitted piece completes before its memory goes away
+  for (auto& k : kids)
+    if (k->rc == BGV_OK) {
+      k->rc = call_wait(&k->call);
+      if (k->rc != BGV_OK && rc == BGV_OK) rc = k->rc;
+    }
+  for (auto& sh : shards)
+    if (sh->rc == BGV_OK) {
+      sh->rc = partial_finish(&sh->call, BGV_OK, sh->codes);
+      if (sh->rc != BGV_OK && rc == BGV_OK) rc = sh->rc;
+    }
+  if (rc != BGV_OK) return rc;
+  bgv_stats st{};
+  for (auto& k : kids) {
+    for (size_t q = 0; q < k->jobs.size(); ++q) out[small[k->j0 + q]] = k->out[q];
+    stats_add(&st, k->st);
+  }
+  for (size_t j = 0; j < njobs; ++j) {
+    if (jobs[j].n_sets < big) continue;
+    int32_t code = 0;
+    bool decided = false;
+    std::vector<uint8_t> parts;
+    for (auto& sh : shards)
+      if (sh->job == j && sh->codes[0] && !decided) {  // first undecodable signature in set order
+        code = sh->codes[0];
+        decided = true;
+      }
+    for (auto& sh : shards)
+      if (sh->job == j && sh->codes[1] && !decided) {  // then the first pubkey condition
+        code = sh->codes[1] == 1 ? -BGV_BLST_PK_IS_INFINITY : sh->codes[1];
+        decided = true;
+      }
+    if (!decided) {
+      for (auto& sh : shards)
+        if (sh->job == j) parts.insert(parts.end(), sh->part, sh->part + 576);
+      int32_t v = 0;
+      const int frc = bgv_final_verify(c, parts.data(), parts.size() / 576, &v);
+      if (frc != BGV_OK) return frc;
+      code = v ? 1 : 0;
+    }
+    out[j] = code;
+    st.sets_verified += jobs[j].n_sets;
+    st.device_groups += 1;
+  }
+  st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) *stats = st;
+  return BGV_OK;
+}
+
+int bgv_set_split(bgv_ctx* c, uint32_t min_sets) {
+  if (!c) return -BGV_E_ARG;
+  c->split_min = min_sets;
+  return BGV_OK;
+}
+
 int bgv_verify(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
                int32_t* out, bgv_stats* stats) {
   if (!c) return -BGV_E_ARG;
+  if (split_wanted(c, nsets)) {
+    if (c->closed) return -BGV_E_CLOSED;
+    if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
+    if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
+    return verify_split(c, jobs, njobs, sets, nsets, mode, out, stats);
+  }
   Call* call = new Call();
   int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, nullptr, nullptr);
   if (rc == BGV_OK) {
@@ -1658,6 +1859,24 @@ int bgv_verify(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* set
 int bgv_verify_async(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
                      int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user) {
   if (!c) return -BGV_E_ARG;
+  if (split_wanted(c, nsets)) {
+    // a split call waits for its pieces and combines them: on a thread of its own (big calls
+    // only), then done() as for any call
+    if (c->closed) return -BGV_E_CLOSED;
+    if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
+    if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
+    c->split_inflight.fetch_add(1);
+    std::thread([=] {
+      const int rc = verify_split(c, jobs, njobs, sets, nsets, mode, out, stats);
+      if (done) done(user, rc);
+      {
+        std::lock_guard<std::mutex> lk(c->split_mu);
+        c->split_inflight.fetch_sub(1);
+      }
+      c->split_cv.notify_all();
+    }).detach();
+    return BGV_OK;
+  }
   Call* call = new Call();
   call->owned = true;  // deleted by the dispatcher after done()
   int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, done, user);
@@ -1670,23 +1889,37 @@ static void fp12_one_bytes(uint8_t out[576]) {
   out[47] = 1;  // c0.c0.c0 = 1, big-endian
 }
 
+// One job's sets -> its Fp12 Miller-loop product and status codes on device dev (-1: any).
+static int partial_submit(bgv_ctx* c, Call* call, const bgv_set* sets, size_t nsets, uint8_t* out576,
+                          int32_t* out_codes, int dev) {
+  out_codes[0] = out_codes[1] = 0;
+  fp12_one_bytes(out576);
+  call->partial_out = out576;
+  call->partial_codes = out_codes;
+  call->pjob = bgv_job{0, (uint32_t)nsets, 0};
+  return call_submit(c, call, &call->pjob, 1, sets, nsets, BGV_MODE_PER_JOB, &call->pcode, nullptr, nullptr, nullptr,
+                     dev);
+}
+
+static int call_wait(Call* call) {
+  std::unique_lock<std::mutex> lk(call->mu);
+  call->cv.wait(lk, [call] { return call->finished; });
+  return call->rc;
+}
+
+static int partial_finish(Call* call, int rc, int32_t* out_codes) {
+  if (rc == BGV_OK) rc = call_wait(call);
+  if (rc == BGV_OK && call->pcode < 0 && call->pcode != -BGV_E_DEVICE) out_codes[0] = call->pcode;  // host-side
+  return rc;
+}
+
 int bgv_verify_partial(bgv_ctx* c, const bgv_set* sets, size_t nsets, uint8_t out576[576], int32_t out_codes[2]) {
   if (!c || !out576 || !out_codes || (nsets && !sets)) return -BGV_E_ARG;
   out_codes[0] = out_codes[1] = 0;
   fp12_one_bytes(out576);
   if (nsets == 0) return c->closed ? -BGV_E_CLOSED : BGV_OK;  // an empty shard: the identity
   Call* call = new Call();
-  call->partial_out = out576;
-  call->partial_codes = out_codes;
-  call->pjob = bgv_job{0, (uint32_t)nsets, 0};
-  int rc = call_submit(c, call, &call->pjob, 1, sets, nsets, BGV_MODE_PER_JOB, &call->pcode, nullptr, nullptr,
-                       nullptr);
-  if (rc == BGV_OK) {
-    std::unique_lock<std::mutex> lk(call->mu);
-    call->cv.wait(lk, [call] { return call->finished; });
-    rc = call->rc;
-    if (rc == BGV_OK && call->pcode < 0 && call->pcode != -BGV_E_DEVICE) out_codes[0] = call->pcode;  // host-side
-  }
+  const int rc = partial_finish(call, partial_submit(c, call, sets, nsets, out576, out_codes, -1), out_codes);
   delete call;
   return rc;
 }

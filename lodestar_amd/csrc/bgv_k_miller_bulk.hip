@@ -7,17 +7,33 @@
 //   k_lines  one lane per twist point Q (each distinct signing root's H, each group's S_g):
 //            walks T over the loop and writes the 68 P-free line records (bls_pairing.h
 //            lz_pline_dbl / lz_pline_add) to HBM.  Live set: T and one step's temporaries.
-//   k_facc   one lane per pair: f <- f^2 * line(P) over the records of its Q, the records
-//            staged through LDS one step ahead (global_load_lds, no VGPRs in flight).  Live
-//            set: f, P's three constants and the step's temporaries.
+//   k_facc   one lane per pair: f <- f^2 * line(P) over the records of its Q.  The records are
+//            staged through LDS: each step's record is read from LDS and the next one's DMA
+//            (global_load_lds_dwordx4, no VGPR destination) issued right after, so it lands
+//            during the line product and the next squaring; P's three constants also wait in
+//            LDS between the steps' scalings.  Live set: f and the step's temporaries.
 //
 // One loop of the single-pass k_miller kept f (168 u32), T (84) and P (42) live across every
 // out-of-line product: 2.7 KB of scratch per lane and 230x its algorithmic HBM bytes
-// (DESIGN.md section 2).  Split, each phase's live set fits the registers the calling
-// convention preserves across a product call.
+// (DESIGN.md section 2).  Split, each phase's live set is smaller.
 //
-// Records: word d of record k (step k of the loop) of pair p is lines[(k * 84 + d) * cap + p]
-// (cap = the buffer's pairs): a wave's 64 lanes read and write 256 consecutive bytes.
+// Records: quad q (words 4q..4q+3) of record k (step k of the loop) of pair p is the 16 bytes at
+// lines[((k * 21 + q) * cap + p) * 4] (cap = the buffer's pairs): a wave's 64 lanes write and
+// read 1 KB contiguously, one dwordx4 instruction per quad.
+// -DBGV_BULK_MILLER_INLINE inlines this unit's Montgomery products (bls_lazy.h
+// BGV_LAZY_INLINE_MUL).  An out-of-line product costs 2,850 SIMD cycles per wave at one wave per
+// SIMD against 2,080 inlined in a tight loop (tools/ubench_prod.hip, profiles/r04/ubench_prod.jsonl),
+// but inlined here the loop bodies grow to ~52k instructions (~400 KB, past the 64 KB
+// instruction cache) and the Miller stage measured 11.6-11.7 ms against 10.8-10.9 ms with calls
+// (profiles/r04/inline_ab/): not the default.
+#ifdef BGV_BULK_MILLER_INLINE
+#define BGV_LAZY_INLINE_MUL 1
+#endif
+// The products of this unit go to the hand-scheduled subroutines (bgv_fpmul_asm.h) through
+// exact-clobber calls; -DBGV_BULK_MILLER_ABI keeps the ABI calls to fp_mul_l (A/B).
+#if !defined(BGV_BULK_MILLER_ABI) && !defined(BGV_BULK_MILLER_INLINE) && !defined(BGV_ASM_MUL)
+#define BGV_ASM_MUL 1
+#endif
 #include "bgv_device.h"
 
 #ifndef BGV_WPE_LINES
@@ -57,11 +73,11 @@ __global__ void BGV_KATTR_LINES k_lines(const bgv_dslot* __restrict__ slots, uin
   } else {
     return;
   }
-  uint32_t* base = lines + p;
+  uint32_t* base = lines + 4 * (size_t)p;
   miller_lines_walk(q, [&](int k, const auto& rec) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(&rec);
-    uint32_t* dst = base + (size_t)k * BGV_LINE_WORDS * cap;
-    BGV_UNROLL for (int d = 0; d < BGV_LINE_WORDS; ++d) dst[(size_t)d * cap] = w[d];
+    const uint4* w = reinterpret_cast<const uint4*>(&rec);
+    uint4* dst = reinterpret_cast<uint4*>(base + (size_t)k * BGV_LINE_QUADS * 4 * cap);
+    BGV_UNROLL for (int d = 0; d < BGV_LINE_QUADS; ++d) dst[(size_t)d * cap] = w[d];
   });
 }
 
@@ -96,11 +112,34 @@ __global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint3
     *out = fp12_one();
     return;
   }
-  const uint32_t* base = lines + lp;
-  *out = miller_facc_walk(*P, [&](int k, auto* rec) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(rec);
-    const uint32_t* src = base + (size_t)k * BGV_LINE_WORDS * cap;
-    BGV_UNROLL for (int d = 0; d < BGV_LINE_WORDS; ++d) w[d] = src[(size_t)d * cap];
+  // this wave's LDS: the staged record [quad][lane] and P's constants [word][lane]
+  __shared__ uint4 rec_lds[BGV_LINE_QUADS][64];
+  __shared__ uint32_t p_lds[3 * NL][64];
+  const int lane = threadIdx.x;
+  const uint32_t* base = lines + 4 * (size_t)lp;
+  auto dma = [&](int k) {  // record k of this lane's pair -> rec_lds (lane-linear, 16 B per lane)
+    const uint32_t* src = base + (size_t)k * BGV_LINE_QUADS * 4 * cap;
+    BGV_UNROLL for (int d = 0; d < BGV_LINE_QUADS; ++d)
+      __builtin_amdgcn_global_load_lds(src + (size_t)d * 4 * cap, &rec_lds[d][0], 16, 0, 0);
+  };
+  dma(0);
+  const miller_p P0 = miller_p_make(*P);
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    p_lds[i][lane] = P0.xn.v[i];
+    p_lds[NL + i][lane] = P0.yp.v[i];
+    p_lds[2 * NL + i][lane] = P0.zp3.v[i];
+  }
+  *out = miller_facc_walk_staged([&](int k, uint32_t z, auto* r) {
+    // record k landed (its DMA was issued one step ago): read it, then stage record k + 1
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    uint4* w = reinterpret_cast<uint4*>(r);
+    BGV_UNROLL for (int d = 0; d < BGV_LINE_QUADS; ++d) w[d] = rec_lds[d][lane + z];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the buffer is free again
+    if (k + 1 < BGV_MILLER_STEPS) dma(k + 1);
+  }, [&](int which, uint32_t z) {  // P's constants from LDS: 0 xn, 1 yp, 2 zp3
+    lzr v;
+    BGV_UNROLL for (int i = 0; i < NL; ++i) v.v[i] = p_lds[which * NL + i][lane + z];
+    return v;
   });
 }
 

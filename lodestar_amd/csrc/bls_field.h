@@ -275,8 +275,26 @@ BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
   return fp_sqr_body(a);
 }
 
+// BGV_ASM_MUL (device code): the products go to the hand-scheduled subroutines of
+// bgv_fpmul_asm.h (tools/gen_fpmul_asm.py) through inline-asm calls with an exact clobber set
+// instead of the ABI calls to fp_mul_l / fp_sqr_l: same limbs, bit for bit.
+#include "bgv_fpmul_asm.h"
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BGV_ASM_MUL)
+#define BGV_USE_ASM_MUL 1
+__device__ __forceinline__ fp_t fp_mul(const fp_t& a, const fp_t& b) {
+  fp_t r = a;
+  bgv_fpmul_asm(r.v, b);
+  return r;
+}
+__device__ __forceinline__ fp_t fp_sqr(const fp_t& a) {
+  fp_t r = a;
+  bgv_fpsqr_asm(r.v);
+  return r;
+}
+#else
 BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_mul_l(BGV_V14(a), BGV_V14(b)); }
 BGV_HD fp_t fp_sqr(const fp_t& a) { return fp_sqr_l(BGV_V14(a)); }
+#endif
 
 // canonical representative in [0, p) of a weakly reduced value
 BGV_HD fp_t fp_canon(const fp_t& a) {

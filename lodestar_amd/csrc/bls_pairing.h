@@ -271,6 +271,7 @@ BGV_HD fp12_t miller_loop1(const g1_jac& p, const g2_jac& q) { return miller_loo
 // ---------------------------------------------------------------------------
 #define BGV_MILLER_STEPS 68
 #define BGV_LINE_WORDS (6 * NL)
+#define BGV_LINE_QUADS (BGV_LINE_WORDS / 4)
 
 template <class A, class B, class C>
 struct lz_pline_t {
@@ -352,6 +353,15 @@ BGV_HD lzf12 lz_facc_add(const lzf12& f, const Lp& L, const lz_mp& P) {
   lz_pline_scale(L, P, &l0, &l1, &l3);
   return lz12_red(lz12_mul_line(f, l0, l1, l3));
 }
+// scaling with P's constants fetched at the point of use (k_facc keeps them in LDS); z is an
+// opaque 0 the fetches depend on, so the compiler cannot hoist them ahead of f^2
+template <class Lp, class PF>
+BGV_HD void lz_pline_scale_f(const Lp& L, PF pget, uint32_t z, lz2r* l0, lz2r* l1, lz2r* l3) {
+  *l0 = lz2_mul_fp(L.L0, pget(2, z));
+  *l1 = lz2_mul_fp(L.L1, pget(0, z));
+  *l3 = lz2_mul_fp(L.L3, pget(1, z));
+}
+
 // A word that is always 0 but depends on every coefficient of f: an index built from it keeps
 // the compiler from issuing a step's record loads before f^2 exists (hoisted, the 84 loaded
 // words stay live across the whole squaring and push f's temporaries into scratch).
@@ -395,6 +405,35 @@ BGV_HD void miller_lines_walk(const g2_jac* qm, Emit emit) {
     }
     emit(k++, lz_pline_dbl(t));
   }
+}
+
+// k_facc's walk with the records and P's constants in LDS: load(k, rec) fills record k,
+// pget(j) returns P's constant j (0 xn = -X Z, 1 yp = Y, 2 zp3 = Z^3).  The record of a
+// doubling is read after f^2 (lz12_after), when only f^2 is live.
+template <class Load, class PF>
+BGV_HD fp12_t miller_facc_walk_staged(Load load, PF pget) {
+  lz2r l0, l1, l3;
+  int k = 0;
+  lz_pline_d d;
+  load(k++, 0u, &d);
+  lz_pline_scale_f(d, pget, 0u, &l0, &l1, &l3);
+  const lz2r z = lz2r{lz_in(fp_zero()), lz_in(fp_zero())};
+  lzf12 f = lzf12{lz6<LMASK, 2>{l0, l1, z}, lz6<LMASK, 2>{z, l3, z}};
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (miller_add_at(i)) {
+      const uint32_t za = lz12_after(f);
+      lz_pline_a a;
+      load(k++, za, &a);
+      lz_pline_scale_f(a, pget, za, &l0, &l1, &l3);
+      f = lz12_red(lz12_mul_line(f, l0, l1, l3));
+    }
+    const lzf12 f2 = lz12_red(lz12_sqr(f));
+    const uint32_t zd = lz12_after(f2);
+    load(k++, zd, &d);
+    lz_pline_scale_f(d, pget, zd, &l0, &l1, &l3);
+    f = lz12_red(lz12_mul_line(f2, l0, l1, l3));
+  }
+  return fp12_conj(lz12_out(f));
 }
 
 // k_facc's walk over one pair's records (load(k, rec) fills record k); returns f, conjugated

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "bgv_verify_async", "bgv_aggregate_pubkeys", "bgv_hash_to_g2", "bgv_keygen", "bgv_sign",
     "bgv_set_rng_seed", "bgv_strerror", "bgv_device_count", "bgv_profile",
     "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify", "bgv_set_batching",
-    "bgv_verify_partial", "bgv_final_verify", "bgv_debug_prepare",
+    "bgv_verify_partial", "bgv_final_verify", "bgv_debug_prepare", "bgv_set_split",
 ]
 
 
@@ -103,6 +103,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_sign": ([P, P, P, SZ, P], ctypes.c_int),
             "bgv_set_rng_seed": ([P, U64], ctypes.c_int),
             "bgv_set_batching": ([P, U32, U32, U32], ctypes.c_int),
+            "bgv_set_split": ([P, U32], ctypes.c_int),
             "bgv_verify_partial": ([P, P, SZ, P, P], ctypes.c_int),
             "bgv_final_verify": ([P, P, SZ, P], ctypes.c_int),
             "bgv_debug_prepare": ([P, P, SZ, ctypes.c_int, U64, P, P, P], ctypes.c_int),
@@ -114,7 +115,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_deposits_verify": ([P, P, P, P, SZ, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
-            if name == "bgv_debug_prepare" and path != os.path.join(HERE, "libblsgpu.so") and \
+            if name in ("bgv_debug_prepare", "bgv_set_split") and path != os.path.join(HERE, "libblsgpu.so") and \
                     not hasattr(lib, name):
                 continue  # parity hook absent from an older A/B build (tools/gpu/ab.sh)
             fn = getattr(lib, name)
@@ -185,6 +186,20 @@ class Context:
                      idle_coalesce_us: int = 0xFFFFFFFF):
         """Super-batch geometry (bgv_set_batching); 0 / 0xFFFFFFFF leave a value unchanged."""
         _check(self.lib.bgv_set_batching(self._h, max_batch_slots, coalesce_us, idle_coalesce_us))
+
+    def set_split(self, min_sets: int):
+        """Calls of at least min_sets sets spread over the context's devices (bgv_set_split;
+        0 disables)."""
+        _check(self.lib.bgv_set_split(self._h, min_sets))
+
+    def verify_packed_one_job(self, packed: "PackedSingleSets", mode: int = MODE_PER_JOB,
+                              stats: Optional[BgvStats] = None) -> int:
+        """One job over all of a PackedSingleSets' sets (bgv_verify): its code."""
+        job = BgvJob(0, packed.nsets, 0)
+        out = (ctypes.c_int32 * 1)()
+        _check(self.lib.bgv_verify(self._h, ctypes.byref(job), 1, packed.ptr(), packed.nsets, mode, out,
+                                   ctypes.byref(stats) if stats is not None else None))
+        return out[0]
 
     def set_rng_seed(self, seed: int):
         _check(self.lib.bgv_set_rng_seed(self._h, seed))

@@ -91,3 +91,92 @@ def test_pubkeys_append_while_verifying():
         assert c.verify_jobs([j], native.MODE_WORKER) == [1]
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------------------------------
+# One call over several devices inside libblsgpu (VERDICT r03 "next" #5):
+# Context([0, 0]) -- two devices of the context, both on the box's one GPU -- spreads calls of
+# at least split_min sets over them (bgv_set_split): a big job as one run per device whose Fp12
+# partials meet in one final exponentiation, the other jobs in runs pinned to each device.
+# Codes must equal the unsplit call's on Context([0]).  Reference split point:
+# packages/beacon-node/src/chain/bls/multithread/index.ts:153-166.
+# ---------------------------------------------------------------------------------------
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _interop_sk(i):
+    import hashlib
+    return (int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R).to_bytes(32, "big")
+
+
+@pytest.fixture(scope="module")
+def split_ctxs():
+    from lodestar_amd import native
+    n = 1 << 20
+    sks = [_interop_sk(i) for i in range(n)]
+    ctxs = []
+    for devs in ([0], [0, 0]):
+        c = native.Context(devs)
+        for lo in range(0, n, 1 << 17):
+            c.keygen(b"".join(sks[lo:lo + (1 << 17)]), cache_first=lo, want_pubkeys=False)
+        ctxs.append(c)
+    ctxs[1].set_split(2048)
+    yield ctxs, sks
+    for c in ctxs:
+        c.close()
+
+
+def _sweep_sets(c, sks, n, seed):
+    import hashlib
+    import random
+    rng = random.Random(seed)
+    idx = rng.sample(range(1 << 20), n) if n < (1 << 20) else list(range(n))
+    roots = [hashlib.sha256(b"split-%d" % (i // 128)).digest() for i in range(n)]
+    sigs = bytearray()
+    for lo in range(0, n, 1 << 17):
+        sigs += c.sign(b"".join(sks[k] for k in idx[lo:lo + (1 << 17)]), b"".join(roots[lo:lo + (1 << 17)]))
+    return idx, roots, bytes(sigs)
+
+
+def test_split_config4_mode_ii(split_ctxs):
+    """8192 sets in one call (config 4 mode (ii)): valid, one wrong message, one bad encoding;
+    also as 8192 batchable one-set jobs (split by jobs) with the same corruptions."""
+    from lodestar_amd import native
+    (one, two), sks = split_ctxs
+    idx, roots, sigs = _sweep_sets(one, sks, 8192, 0x8192)
+    base = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[idx[i]]) for i in range(8192)]
+    wrong = list(base)
+    wrong[5000] = native.SetSpec(roots[4000 - 128], base[5000].sig, pk_indices=[idx[5000]])
+    bad = list(base)
+    bad[7000] = native.SetSpec(roots[7000], bytes([base[7000].sig[0] & 0x7F]) + base[7000].sig[1:],
+                               pk_indices=[idx[7000]])
+    for sets, want in ((base, 1), (wrong, 0), (bad, -native.BLST_BAD_ENCODING)):
+        got = [c.verify_jobs([(sets, False)], native.MODE_WORKER) for c in (one, two)]
+        assert got == [[want], [want]]
+        per = [c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER) for c in (one, two)]
+        assert per[0] == per[1]
+        assert sum(1 for v in per[0] if v != 1) == (0 if want == 1 else 1)
+
+
+def test_split_epoch_sweep_2p20(split_ctxs):
+    """The config-5 sweep as one job: 2^20 single sets over the 2^20-key cache, valid, with two
+    signatures swapped (false), and with one undecodable signature (BLST_BAD_ENCODING)."""
+    from lodestar_amd import native
+    (one, two), sks = split_ctxs
+    n = 1 << 20
+    idx, roots, sigs = _sweep_sets(one, sks, n, 0)
+    packed = native.PackedSingleSets(b"".join(roots), sigs, idx)
+    assert one.verify_packed_one_job(packed) == 1
+    st = native.BgvStats()
+    assert two.verify_packed_one_job(packed, stats=st) == 1
+    assert st.sets_verified == n
+    swapped = bytearray(sigs)
+    a, b = 1000, 900000
+    swapped[96 * a:96 * a + 96], swapped[96 * b:96 * b + 96] = sigs[96 * b:96 * b + 96], sigs[96 * a:96 * a + 96]
+    packed = native.PackedSingleSets(b"".join(roots), bytes(swapped), idx)
+    assert [one.verify_packed_one_job(packed), two.verify_packed_one_job(packed)] == [0, 0]
+    broken = bytearray(sigs)
+    broken[96 * 777777] &= 0x7F
+    packed = native.PackedSingleSets(b"".join(roots), bytes(broken), idx)
+    want = -native.BLST_BAD_ENCODING
+    assert [one.verify_packed_one_job(packed), two.verify_packed_one_job(packed)] == [want, want]

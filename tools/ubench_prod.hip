@@ -4,12 +4,15 @@
 //   body   fp_mul_body inlined (the compiler's column schedule)
 //   split  each column's product sum in two interleaved accumulators (even / odd rows), the
 //          reduction rows as in fp_mul_body: more independent mad chains in flight
+//   split_call  the split product out of line (fp_mul_l's argument convention)
+//   asm_call    the hand-scheduled subroutine of bgv_fpmul_asm.h (exact clobbers, no ABI)
 // Products/s and the implied cycles per product per wave.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ubench_prod tools/ubench_prod.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 
+#define BGV_ASM_EMIT 1
 #include "../lodestar_amd/csrc/bls_field.h"
 
 #define CHECK(x)                                                                             \
@@ -58,11 +61,42 @@ __device__ __forceinline__ fp_t mul_split(const fp_t& a, const fp_t& b) {
   return r;
 }
 
+// the split schedule out of line, with fp_mul_l's argument convention
+static __device__ __noinline__ fp_t mul_split_l(BGV_U14(a_), BGV_U14(b_)) {
+  const fp_t a = {{BGV_L14(a_)}}, b = {{BGV_L14(b_)}};
+  return mul_split(a, b);
+}
+
 template <int V>
 __device__ __forceinline__ fp_t prod(const fp_t& a, const fp_t& b) {
   if constexpr (V == 0) return fp_mul(a, b);
   if constexpr (V == 1) return fp_mul_body(a, b);
-  return mul_split(a, b);
+  if constexpr (V == 2) return mul_split(a, b);
+  if constexpr (V == 3) return mul_split_l(BGV_V14(a), BGV_V14(b));
+  fp_t r = a;  // V == 4: the hand-scheduled subroutine (bgv_fpmul_asm.h)
+  bgv_fpmul_asm(r.v, b);
+  return r;
+}
+
+// bit-exactness of the subroutines against fp_mul_body / fp_sqr_body on lane-varying operands
+__global__ void __launch_bounds__(64) k_check(uint32_t* bad, uint32_t seed) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t x = seed ^ (tid * 2654435761u);
+  auto rnd = [&x] { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+  fp_t a, b;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    a.v[i] = rnd() & 0x1fffffff;
+    b.v[i] = rnd() & 0x1fffffff;
+  }
+  a.v[NL - 1] &= 0x7ffff;
+  b.v[NL - 1] &= 0x7ffff;
+  fp_t m = a, q = a;
+  bgv_fpmul_asm(m.v, b);
+  bgv_fpsqr_asm(q.v);
+  const fp_t m0 = fp_mul_body(a, b), q0 = fp_sqr_body(a);
+  uint32_t diff = 0;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) diff |= (m.v[i] ^ m0.v[i]) | (q.v[i] ^ q0.v[i]);
+  if (diff) atomicAdd(bad, 1u);
 }
 
 template <int V, int CHAINS>
@@ -114,6 +148,15 @@ int main() {
   const int cus = prop.multiProcessorCount;
   uint32_t* d;
   CHECK(hipMalloc(&d, sizeof(uint32_t) * cus * 4 * 2 * 64));
+  {
+    uint32_t bad = 0;
+    CHECK(hipMemset(d, 0, 4));
+    for (uint32_t s = 1; s <= 16; ++s) hipLaunchKernelGGL(k_check, dim3(cus * 4), dim3(64), 0, 0, d, s);
+    CHECK(hipMemcpy(&bad, d, 4, hipMemcpyDeviceToHost));
+    printf("{\"check\": \"asm products vs fp_mul_body / fp_sqr_body\", \"lanes\": %d, \"mismatches\": %u}\n",
+           cus * 4 * 64 * 16, bad);
+    if (bad) return 1;
+  }
   for (int wps : {1, 2}) {
     run<0, 1>("call", d, cus, wps);
     run<0, 2>("call", d, cus, wps);
@@ -121,6 +164,10 @@ int main() {
     run<1, 2>("body", d, cus, wps);
     run<2, 1>("split", d, cus, wps);
     run<2, 2>("split", d, cus, wps);
+    run<3, 1>("split_call", d, cus, wps);
+    run<3, 2>("split_call", d, cus, wps);
+    run<4, 1>("asm_call", d, cus, wps);
+    run<4, 2>("asm_call", d, cus, wps);
   }
   CHECK(hipFree(d));
   return 0;
