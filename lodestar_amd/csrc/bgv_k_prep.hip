@@ -15,6 +15,7 @@
 #include "bgv_team_dev.h"
 #include "bgv_tcurve.h"
 #include "bgv_tround_dev.h"
+#include "bgv_wfp.h"
 
 static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
 
@@ -130,22 +131,31 @@ __device__ __forceinline__ g2_aff* split_sig(fp12_t* f, uint32_t s) {
 }
 static_assert(sizeof(g2_jac) + sizeof(g2_aff) <= sizeof(fp12_t), "split intermediates fit in f[s]");
 
-// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), isogeny included
-__device__ __noinline__ void task_map(uint32_t s, int which, const bgv_dslot* __restrict__ slots, g2_jac* out) {
+extern "C++" {
+// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), isogeny included.  PW: the
+// square roots' exponentiations on this lane (bgv_pow_lane) or on the whole wave (bgv_pow_wave,
+// one set per wave, every lane computing the same values; lane 0 writes).
+template <class PW>
+__device__ __noinline__ void task_map_t(uint32_t s, int which, const bgv_dslot* __restrict__ slots, g2_jac* out,
+                                        bool writer) {
   const bgv_dslot& d = slots[s];
   if (d.flags & BGV_SLOT_PAD) return;
   uint8_t msg[32];
   for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, 32);
-  *out = iso_map_g2_jac(sswu_g2_jac(which ? u1 : u0, fp_sqrt_minus5()));
+  const g2_jac q = iso_map_g2_jac(sswu_g2_jac_t<PW>(which ? u1 : u0, fp_sqrt_minus5()));
+  if (writer) *out = q;
 }
 
 // task_sig's decoding half: status, and the affine point when it decodes to a finite point
-__device__ __noinline__ void task_sig_decode(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* out,
-                                             int32_t* __restrict__ sig_status) {
+template <class PW>
+__device__ __noinline__ void task_sig_decode_t(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* out,
+                                               int32_t* __restrict__ sig_status, bool writer) {
   const bgv_dslot& d = slots[s];
   int32_t st = BGV_ST_OK;
+  g2_aff a;
+  bool fin = false;
   if (d.flags & BGV_SLOT_PAD) {
     st = BGV_ST_INFINITY;
   } else if (d.sig_len != 96) {
@@ -153,18 +163,21 @@ __device__ __noinline__ void task_sig_decode(uint32_t s, const bgv_dslot* __rest
   } else {
     uint8_t b[96];
     for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
-    g2_aff a;
     bool inf;
-    st = g2_decompress(&a, &inf, b);
+    st = g2_decompress_t<PW>(&a, &inf, b);
     if (st == BGV_OK) {
       if (inf)
         st = BGV_ST_INFINITY;
       else
-        *out = a;
+        fin = true;
     }
   }
-  sig_status[s] = st;
+  if (writer) {
+    if (fin) *out = a;
+    sig_status[s] = st;
+  }
 }
+}  // extern "C++"
 
 // merged (the smallest calls, with k_prep_wide): plane 3 sums committee-sized sets' cached
 // keys (k_pk_agg16's teams), plane 4 larger sets' (k_pk_agg's wave tree), and k_prep_wide
@@ -184,14 +197,25 @@ __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uin
     }
     return;
   }
+  if (merged) {  // one set per wave (grid.x = nslots): the square roots on the whole wave
+    const uint32_t s = blockIdx.x;
+    const bool w = threadIdx.x == 0;
+    if (blockIdx.y == 0)
+      task_map_t<bgv_pow_wave>(s, 0, slots, h + s, w);
+    else if (blockIdx.y == 1)
+      task_map_t<bgv_pow_wave>(s, 1, slots, split_q1(f, s), w);
+    else
+      task_sig_decode_t<bgv_pow_wave>(s, slots, split_sig(f, s), sig_status, w);
+    return;
+  }
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   if (blockIdx.y == 0)
-    task_map(s, 0, slots, h + s);
+    task_map_t<bgv_pow_lane>(s, 0, slots, h + s, true);
   else if (blockIdx.y == 1)
-    task_map(s, 1, slots, split_q1(f, s));
+    task_map_t<bgv_pow_lane>(s, 1, slots, split_q1(f, s), true);
   else if (blockIdx.y == 2)
-    task_sig_decode(s, slots, split_sig(f, s), sig_status);
+    task_sig_decode_t<bgv_pow_lane>(s, slots, split_sig(f, s), sig_status, true);
   else
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
 }

@@ -419,8 +419,10 @@ enum {
 };
 
 // 96-byte compressed G2 (signature) -> affine; *inf set for the infinity
-// encoding.  Mirrors blst_p2_uncompress; returns a BGV_* code.
-BGV_HD int g2_decompress(g2_aff* out, bool* inf, const uint8_t* b) {
+// encoding.  Mirrors blst_p2_uncompress; returns a BGV_* code.  PW: the square root's
+// exponentiation policy (bls_field.h bgv_pow_lane / bgv_wfp.h bgv_pow_wave).
+template <class PW>
+BGV_HD int g2_decompress_t(g2_aff* out, bool* inf, const uint8_t* b) {
   const uint8_t flags = b[0];
   *inf = false;
   if (!(flags & 0x80)) return BGV_BAD_ENCODING;
@@ -441,13 +443,14 @@ BGV_HD int g2_decompress(g2_aff* out, bool* inf, const uint8_t* b) {
   const fp2_t B = BGV_B2;
   fp2_t y2 = fp2_add(fp2_mul(fp2_sqr(x), x), B);
   fp2_t y;
-  if (!fp2_sqrt(&y, y2)) return BGV_POINT_NOT_ON_CURVE;
+  if (!fp2_sqrt_t<PW>(&y, y2)) return BGV_POINT_NOT_ON_CURVE;
   const bool want = (flags & 0x20) != 0;
   if (fp2_lex_largest(y) != want) y = fp2_neg(y);
   out->x = x;
   out->y = y;
   return BGV_OK;
 }
+BGV_HD int g2_decompress(g2_aff* out, bool* inf, const uint8_t* b) { return g2_decompress_t<bgv_pow_lane>(out, inf, b); }
 
 BGV_HD void g2_compress(uint8_t* b, const g2_aff& a, bool inf) {
   if (inf) {

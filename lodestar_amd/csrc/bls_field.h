@@ -420,12 +420,22 @@ BGV_HD fp_t fp_inv(const fp_t& a) { return fp_pow_fixed<BGV_POW_INV>(a); }
 // a^((p-3)/4): for a QR, a * t = sqrt(a) and t = 1/sqrt(a).
 BGV_HD fp_t fp_pow_p_minus_3_div_4(const fp_t& a) { return fp_pow_fixed<BGV_POW_P34>(a); }
 
+// The fixed exponentiations of the square roots, as a policy: bgv_pow_lane runs them on the
+// calling lane; bgv_wfp.h's bgv_pow_wave spreads each product over the wavefront (the latency
+// path, one set per wave).  Same schedules, same values.
+struct bgv_pow_lane {
+  static BGV_HD fp_t p34(const fp_t& a) { return fp_pow_fixed<BGV_POW_P34>(a); }
+  static BGV_HD fp_t sqrt_exp(const fp_t& a) { return fp_pow_fixed<BGV_POW_SQRT>(a); }
+};
+
 // sqrt candidate; returns true iff a is a square (then *out = a^((p+1)/4)).
-BGV_HD bool fp_sqrt(fp_t* out, const fp_t& a) {
-  fp_t s = fp_pow_fixed<BGV_POW_SQRT>(a);
+template <class PW>
+BGV_HD bool fp_sqrt_t(fp_t* out, const fp_t& a) {
+  fp_t s = PW::sqrt_exp(a);
   *out = s;
   return fp_eq(fp_sqr(s), a);
 }
+BGV_HD bool fp_sqrt(fp_t* out, const fp_t& a) { return fp_sqrt_t<bgv_pow_lane>(out, a); }
 
 // a / 2 mod p (a weakly reduced; the limb-0 parity is the value's parity)
 BGV_HD fp_t fp_half(const fp_t& a) {
@@ -549,14 +559,15 @@ BGV_HD fp2_t fp2_half(const fp2_t& a) { return fp2_t{fp_half(a.c0), fp_half(a.c1
 // Square root in Fp2 (p = 3 mod 4) by the norm ("complex") method with one
 // shared exponentiation for sqrt and inverse.  Returns false if a is not a
 // square.  Any root is returned; callers fix the sign.
-BGV_NOINLINE bool fp2_sqrt(fp2_t* out, const fp2_t& a) {
+template <class PW>
+BGV_NOINLINE bool fp2_sqrt_t(fp2_t* out, const fp2_t& a) {
   const fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   fp_t g;
-  const bool n_sq = fp_sqrt(&g, n);
+  const bool n_sq = fp_sqrt_t<PW>(&g, n);
   const bool a1z = fp_is_zero(a.c1);
   // delta = a1 == 0 ? a0 : (a0 + g) / 2
   fp_t d = fp_select(a1z, fp_half(fp_add(a.c0, g)), a.c0);
-  fp_t t = fp_pow_p_minus_3_div_4(d);
+  fp_t t = PW::p34(d);
   fp_t dt = fp_mul(d, t);
   fp_t s = fp_mul(dt, t);  // d^((p-1)/2)
   fp_t a1t2 = fp_half(fp_mul(a.c1, t));
@@ -568,6 +579,7 @@ BGV_NOINLINE bool fp2_sqrt(fp2_t* out, const fp2_t& a) {
   *out = y;
   return n_sq && fp2_eq(fp2_sqr(y), a);
 }
+BGV_HD bool fp2_sqrt(fp2_t* out, const fp2_t& a) { return fp2_sqrt_t<bgv_pow_lane>(out, a); }
 
 // RFC 9380 sgn0 for Fp2 (on raw values)
 BGV_HD uint32_t fp2_sgn0(const fp2_t& a_mont) {

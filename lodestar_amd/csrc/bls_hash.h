@@ -275,7 +275,8 @@ BGV_NOINLINE g2_jac iso_map_g2(const fp2_t& x, const fp2_t& y) {
 //     d^((p+1)/4) = d' T,   h1 d^((p-3)/4) = h1' T,   d^((p-1)/2) = d' n T^2
 // (n^(p-1) = 1), so the same two (p-3)/4 exponentiations as sqrt(g) give sqrt(U/V) and
 // the inversion of the affine map is gone.  The same point as sswu_g2 (tests/test_hostsim_math.py).
-BGV_NOINLINE g2_jac sswu_g2_jac(const fp2_t& u, const fp_t& sqrt_m5) {
+template <class PW>
+BGV_NOINLINE g2_jac sswu_g2_jac_t(const fp2_t& u, const fp_t& sqrt_m5) {
   const fp2_t Z = BGV_SSWU_Z, A = BGV_SSWU_A, B = BGV_SSWU_B;
   const fp2_t tv1 = fp2_mul(Z, fp2_sqr(u));
   const fp2_t tv2 = fp2_add(fp2_sqr(tv1), tv1);
@@ -288,13 +289,13 @@ BGV_NOINLINE g2_jac sswu_g2_jac(const fp2_t& u, const fp_t& sqrt_m5) {
   const fp2_t w = fp2_mul(U, fp2_conj(V));
   const fp_t n = fp_add(fp_sqr(V.c0), fp_sqr(V.c1));
   const fp_t nw = fp_add(fp_sqr(w.c0), fp_sqr(w.c1));
-  const fp_t e = fp_pow_p_minus_3_div_4(nw);
+  const fp_t e = PW::p34(nw);
   const fp_t ne = fp_mul(nw, e);
   const bool sq = fp_eq(fp_mul(ne, e), fp_one()) || fp_is_zero(nw);
   const fp2_t h = fp2_select(sq, fp2_mul(Z, w), w);
   const fp_t gam = fp_select(sq, fp_mul(sqrt_m5, fp_neg(ne)), ne);
   const fp_t d = fp_select(fp_is_zero(h.c1), fp_half(fp_add(h.c0, gam)), h.c0);
-  const fp_t T = fp_mul(n, fp_pow_p_minus_3_div_4(fp_mul(d, fp_mul(fp_sqr(n), n))));
+  const fp_t T = fp_mul(n, PW::p34(fp_mul(d, fp_mul(fp_sqr(n), n))));
   const fp_t y0 = fp_mul(d, T), y1 = fp_half(fp_mul(h.c1, T));
   const bool qr = fp_eq(fp_mul(fp_mul(d, n), fp_sqr(T)), fp_one());
   fp2_t r;  // sqrt(gx1), or sqrt(Z gx1) when gx1 is not a square
@@ -310,6 +311,7 @@ BGV_NOINLINE g2_jac sswu_g2_jac(const fp2_t& u, const fp_t& sqrt_m5) {
   o.z = x1d;
   return o;
 }
+BGV_HD g2_jac sswu_g2_jac(const fp2_t& u, const fp_t& sqrt_m5) { return sswu_g2_jac_t<bgv_pow_lane>(u, sqrt_m5); }
 
 // 3-isogeny E2' -> E2 (RFC 9380 E.3) of a Jacobian point: the rational maps in x = X/Z^2
 // homogenized with z2 = Z^2 (XN = xnum z2^3, XD = xden z2^2, YN = ynum z2^3, YD = yden z2^3),

@@ -9,6 +9,7 @@
 #   trace    rocprofv3 --kernel-trace --stats of the bench command   -> OUTDIR/bench_trace/
 #   roof     rocprofv3 --kernel-trace --stats of the isolated roofline call -> OUTDIR/roof_trace/
 #   pmc      the PMC passes of the roofline call (tools/gpu/pmc.sh)  -> gpurun_out/<basename OUTDIR>/pmc
+#   latency  config-3 latency probe under a kernel trace              -> OUTDIR/config3_p50.json, lat_trace/
 #   gossip   Node 64-caller gossip bench                             -> OUTDIR/gossip.jsonl
 #   ubench   the VALU / product microbenchmarks                      -> OUTDIR/ubench_*.jsonl
 set -o pipefail
@@ -45,12 +46,17 @@ for step in "$@"; do
       cat "$O/roof_call.json" ;;
     pmc)
       TAG=$(basename "$O") bash tools/gpu/pmc.sh || fail pmc $? /dev/null ;;
+    latency)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/lat_trace" -o run --output-format csv \
+        -- python3 tools/gpu/latency_probe.py 30 > "$O/config3_p50.json" 2> "$O/lat.err" \
+        || fail latency $? "$O/lat.err"
+      cat "$O/config3_p50.json" ;;
     gossip)
       timeout -k 10 200 node tests/node/gossip_bench.js 5 64 > "$O/gossip.jsonl" 2> "$O/gossip.err" \
         || fail gossip $? "$O/gossip.err"
       cat "$O/gossip.jsonl" ;;
     ubench)
-      for u in ubench_valu ubench_fpmul ubench_prod; do
+      for u in ubench_valu ubench_fpmul ubench_prod ubench_wfp; do
         [ -x tools/$u ] || continue
         timeout -k 10 120 tools/$u > "$O/$u.jsonl" 2>&1 || fail $u $? "$O/$u.jsonl"
       done ;;
