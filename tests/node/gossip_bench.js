@@ -4,8 +4,11 @@
 // concurrent callers each validate one single-set batchable attestation at a time
 // (verifySignatureSets([set], {batchable: true}), as validateGossipAttestation does), for
 // `seconds`, over one verifier.  Prints one JSON line per buffering setting with sets/s and
-// per-call latency percentiles.
-//   node gossip_bench.js [seconds=8] [callers=64] [settings="63:1,64:1,32:100,16:1"]
+// per-call latency percentiles.  backend "cpu": the same callers over CpuPoolVerifier (the
+// C++ restatement of the verify path behind BlsMultiThreadWorkerPool's buffering, `workers`
+// packages at once) -- the like-for-like CPU row.
+//   node gossip_bench.js [seconds=8] [callers=64] [settings="63:1,64:1,32:100,16:1"] [backend=gpu|cpu] [workers=16]
+process.env.UV_THREADPOOL_SIZE = process.env.UV_THREADPOOL_SIZE || "32"; // before any async work
 const path = require("path");
 const crypto = require("crypto");
 const {BlsGpuVerifier, addon} = require(path.join(__dirname, "..", "..", "lodestar_amd", "node", "BlsGpuVerifier.js"));
@@ -13,6 +16,8 @@ const {BlsGpuVerifier, addon} = require(path.join(__dirname, "..", "..", "lodest
 const seconds = Number(process.argv[2] || 8);
 const callers = Number(process.argv[3] || 64);
 const settings = (process.argv[4] || "63:1,64:1,32:100,16:1").split(",").map((s) => s.split(":").map(Number));
+const backend = process.argv[5] || "gpu";
+const workers = Number(process.argv[6] || 16);
 const NKEYS = 16384;
 
 function pct(xs, p) {
@@ -20,8 +25,8 @@ function pct(xs, p) {
   return s[Math.min(s.length - 1, Math.floor(p * s.length))];
 }
 
-async function runOne(ctx, sets, maxBufferedSigs, maxBufferWaitMs, secs = seconds) {
-  const v = new BlsGpuVerifier({ctx, maxBufferedSigs, maxBufferWaitMs});
+async function runOne(ctx, sets, maxBufferedSigs, maxBufferWaitMs, secs = seconds, make = null) {
+  const v = make ? make() : new BlsGpuVerifier({ctx, maxBufferedSigs, maxBufferWaitMs});
   let next = 0;
   let done = 0;
   let bad = 0;
@@ -70,9 +75,24 @@ async function main() {
   for (let i = 0; i < NKEYS; i++) {
     sets.push({type: "single", pubkey: i, signingRoot: msgs.slice(32 * i, 32 * i + 32), signature: sigs.slice(96 * i, 96 * i + 96)});
   }
+  if (backend === "cpu") {
+    const {CpuPoolVerifier, loadAddon} = require(path.join(__dirname, "CpuPoolVerifier.js"));
+    const cpu = loadAddon();
+    const pubkeys96 = cpu.skToPk96(sks);
+    const make = () => new CpuPoolVerifier({cpu, pubkeys96, workers});
+    await runOne(ctx, sets, 32, 100, 1, make); // warm-up
+    const r = await runOne(ctx, sets, 32, 100, seconds, make);
+    r.backend = "cpu-port";
+    r.workers = workers;
+    process.stdout.write(JSON.stringify(r) + "\n");
+    addon.close(ctx);
+    return;
+  }
   await runOne(ctx, sets, 32, 2, 2); // warm-up: first launches load code objects
   for (const [b, w] of settings) {
-    process.stdout.write(JSON.stringify(await runOne(ctx, sets, b, w)) + "\n");
+    const r = await runOne(ctx, sets, b, w);
+    r.backend = "gpu";
+    process.stdout.write(JSON.stringify(r) + "\n");
   }
   addon.close(ctx);
 }

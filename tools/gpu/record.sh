@@ -11,6 +11,7 @@
 #   pmc      the PMC passes of the roofline call (tools/gpu/pmc.sh)  -> gpurun_out/<basename OUTDIR>/pmc
 #   latency  config-3 latency probe under a kernel trace              -> OUTDIR/config3_p50.json, lat_trace/
 #   gossip   Node 64-caller gossip bench                             -> OUTDIR/gossip.jsonl
+#   gossip_cpu  the same callers over the C++ port (CpuPoolVerifier, 16 workers) -> OUTDIR/gossip_cpu.jsonl
 #   ubench   the VALU / product microbenchmarks                      -> OUTDIR/ubench_*.jsonl
 set -o pipefail
 O=$1; shift
@@ -55,6 +56,11 @@ for step in "$@"; do
       timeout -k 10 200 node tests/node/gossip_bench.js 5 64 > "$O/gossip.jsonl" 2> "$O/gossip.err" \
         || fail gossip $? "$O/gossip.err"
       cat "$O/gossip.jsonl" ;;
+    gossip_cpu)
+      python tests/node/build_cpu.py > /dev/null || fail build_cpu $? /dev/null
+      timeout -k 10 200 node tests/node/gossip_bench.js 8 64 "" cpu 16 > "$O/gossip_cpu.jsonl" 2> "$O/gossip_cpu.err" \
+        || fail gossip_cpu $? "$O/gossip_cpu.err"
+      cat "$O/gossip_cpu.jsonl" ;;
     ubench)
       for u in ubench_valu ubench_fpmul ubench_prod ubench_wfp; do
         [ -x tools/$u ] || continue
