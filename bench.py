@@ -589,7 +589,7 @@ def epoch_sweep(ctx, native, barrier, rank, world, nsets=EPOCH_SETS, committee=E
 
 
 # PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
-TRAFFIC_FILE = os.path.join("profiles", "r03", "traffic.json")
+TRAFFIC_FILE = os.path.join("profiles", "r04", "traffic.json")
 ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
 
 
