@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libblsgpu.so")
 # kernel translation units (compiled in parallel; each carries its own copy of the
 # out-of-line arithmetic with its own register budget) and the host orchestration
-KERNEL_UNITS = ["bgv_k_prep_bulk.hip", "bgv_k_miller_bulk.hip", "bgv_k_prep.hip", "bgv_k_miller.hip", "bgv_k_final.hip", "bgv_k_util.hip"]
+KERNEL_UNITS = ["bgv_k_prep_bulk.hip", "bgv_k_miller_bulk.hip", "bgv_k_prep.hip", "bgv_k_prep_wave.hip", "bgv_k_miller.hip", "bgv_k_final.hip", "bgv_k_util.hip"]
 SOURCES = [os.path.join(CSRC, f) for f in KERNEL_UNITS] + [os.path.join(CSRC, "bgv_api.cpp")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("BGV_OFFLOAD_ARCH", "gfx950")

@@ -11,11 +11,10 @@
 //              signature's decompression, the pubkey task; (team) the cofactor clearing of
 //              q0 + q1 and r_i * sig_i on 16-lane teams, the subgroup check on one lane
 //   k_prep     (bgv_k_prep_bulk.hip) sig, hash and pk tasks side by side for larger calls
-#include "bgv_k_tasks.h"
+#include "bgv_k_lat.h"
 #include "bgv_team_dev.h"
 #include "bgv_tcurve.h"
 #include "bgv_tround_dev.h"
-#include "bgv_wfp.h"
 
 static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
 
@@ -122,67 +121,10 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   if (blockIdx.x < nslots) pk_aggw_body(slots, blockIdx.x, pk_idx, cache, pk_agg);
 }
 
-// ---- latency path ------------------------------------------------------------------------
-// f[s] (576 B, written by k_miller only later) holds the split's intermediates:
-// q1 = the u1 map's point (g2_jac, 288 B) at offset 0, the decoded signature (g2_aff) at 288.
-__device__ __forceinline__ g2_jac* split_q1(fp12_t* f, uint32_t s) { return reinterpret_cast<g2_jac*>(f + s); }
-__device__ __forceinline__ g2_aff* split_sig(fp12_t* f, uint32_t s) {
-  return reinterpret_cast<g2_aff*>(reinterpret_cast<uint8_t*>(f + s) + sizeof(g2_jac));
-}
-static_assert(sizeof(g2_jac) + sizeof(g2_aff) <= sizeof(fp12_t), "split intermediates fit in f[s]");
-
-extern "C++" {
-// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), isogeny included.  PW: the
-// square roots' exponentiations on this lane (bgv_pow_lane) or on the whole wave (bgv_pow_wave,
-// one set per wave, every lane computing the same values; lane 0 writes).
-template <class PW>
-__device__ __noinline__ void task_map_t(uint32_t s, int which, const bgv_dslot* __restrict__ slots, g2_jac* out,
-                                        bool writer) {
-  const bgv_dslot& d = slots[s];
-  if (d.flags & BGV_SLOT_PAD) return;
-  uint8_t msg[32];
-  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
-  fp2_t u0, u1;
-  hash_to_field_fp2(&u0, &u1, msg, 32);
-  const g2_jac q = iso_map_g2_jac(sswu_g2_jac_t<PW>(which ? u1 : u0, fp_sqrt_minus5()));
-  if (writer) *out = q;
-}
-
-// task_sig's decoding half: status, and the affine point when it decodes to a finite point
-template <class PW>
-__device__ __noinline__ void task_sig_decode_t(uint32_t s, const bgv_dslot* __restrict__ slots, g2_aff* out,
-                                               int32_t* __restrict__ sig_status, bool writer) {
-  const bgv_dslot& d = slots[s];
-  int32_t st = BGV_ST_OK;
-  g2_aff a;
-  bool fin = false;
-  if (d.flags & BGV_SLOT_PAD) {
-    st = BGV_ST_INFINITY;
-  } else if (d.sig_len != 96) {
-    st = BGV_INVALID_SIZE;
-  } else {
-    uint8_t b[96];
-    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
-    bool inf;
-    st = g2_decompress_t<PW>(&a, &inf, b);
-    if (st == BGV_OK) {
-      if (inf)
-        st = BGV_ST_INFINITY;
-      else
-        fin = true;
-    }
-  }
-  if (writer) {
-    if (fin) *out = a;
-    sig_status[s] = st;
-  }
-}
-}  // extern "C++"
-
-// merged (the smallest calls, with k_prep_wide): plane 3 sums committee-sized sets' cached
-// keys (k_pk_agg16's teams), plane 4 larger sets' (k_pk_agg's wave tree), and k_prep_wide
-// does the pubkey task after them; the key trees then overlap the hash and decode planes
-// instead of running before them.  Otherwise plane 3 is the pubkey task.
+// merged (the smallest calls, with k_prep_a_wave and k_prep_wide): only planes 3 and 4 run
+// here -- plane 3 sums committee-sized sets' cached keys (k_pk_agg16's teams), plane 4 larger
+// sets' (k_pk_agg's wave tree) -- and k_prep_wide does the pubkey task after them.
+// Otherwise planes 0..2 are the maps and the decoding, one lane per set, plane 3 the pubkey task.
 __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
                                         fp12_t* __restrict__ f, int32_t* __restrict__ sig_status,
                                         const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
@@ -197,17 +139,7 @@ __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uin
     }
     return;
   }
-  if (merged) {  // one set per wave (grid.x = nslots): the square roots on the whole wave
-    const uint32_t s = blockIdx.x;
-    const bool w = threadIdx.x == 0;
-    if (blockIdx.y == 0)
-      task_map_t<bgv_pow_wave>(s, 0, slots, h + s, w);
-    else if (blockIdx.y == 1)
-      task_map_t<bgv_pow_wave>(s, 1, slots, split_q1(f, s), w);
-    else
-      task_sig_decode_t<bgv_pow_wave>(s, slots, split_sig(f, s), sig_status, w);
-    return;
-  }
+  if (merged) return;  // planes 0..2 ran in k_prep_a_wave (bgv_k_prep_wave.hip)
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   if (blockIdx.y == 0)
@@ -433,8 +365,11 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   const bool wide = bgv_use_latency(b, n + b.ngroups) && n <= BGV_PREP_WIDE_MAX;
   if (wide) {
     const g1_aff* cache = reinterpret_cast<const g1_aff*>(b.cache_opaque);
-    hipLaunchKernelGGL(k_prep_a, dim3(n, 5), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status, b.pk_idx,
-                       cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr, 1);
+    const hipError_t e = bgv_launch_prep_wave(b, s.main);
+    if (e != hipSuccess) return e;
+    if (tree)  // the pubkey trees (planes 3, 4; planes 0..2 exit at once)
+      hipLaunchKernelGGL(k_prep_a, dim3(n, 5), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status, b.pk_idx,
+                         cache, b.pk_bytes, b.rpk, b.pk_status, b.pk_agg, 1);
     hipLaunchKernelGGL(k_prep_wide, dim3(n, 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
                        b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
     BGV_MARK(1);

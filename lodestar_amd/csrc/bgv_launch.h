@@ -80,6 +80,7 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s);  // pr
 bool bgv_sig_pairs(const bgv_dev_batch& b);
 hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s);
 hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bool tree);  // bgv_k_prep_bulk.hip
+hipError_t bgv_launch_prep_wave(const bgv_dev_batch& b, hipStream_t st);  // bgv_k_prep_wave.hip
 hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s);
 // bulk path: k_lines + k_facc over the set pairs and the first ngroups group pairs
 hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipStream_t st);

@@ -187,6 +187,63 @@ __device__ __forceinline__ uint32_t wfp_mul3(uint32_t a, uint32_t b, const wfp_c
   return c.lane < NL ? res : 0u;
 }
 
+// A product of two WAVE-UNIFORM fp_t values (every lane holds the same a and b) on the whole
+// wave, returning the uniform product (normalized limbs): the drop-in for fp_mul in code that
+// runs one set per wave.  Same three lane-parallel products as wfp_mul3, arranged so that no
+// per-wave constants are needed: a.b takes a's limbs straight from the (uniform) VGPRs and b
+// rotated; t N' and m p take N' and p as scalar constants and rotate t and m instead (lane L
+// reads lane L - j: wave_ror steps; t and m are masked to lanes 50..63, so terms outside a
+// column's range read 0).  The value equals fp_mul_body's: (ab + mp) / R with m = -ab/p mod R.
+__device__ __noinline__ fp_t wfp_umul(const fp_t a, const fp_t b) {
+  const uint32_t lane = wfp_lane();
+  const bool low = lane >= 50;
+  uint32_t r = 0;
+  BGV_UNROLL for (int l = 0; l < NL; ++l) r = lane == (uint32_t)l ? b.v[l] : r;
+  uint32_t br[NL];
+  BGV_UNROLL for (int k = 1; k <= NL; ++k) {
+    r = wfp_rol1(r);
+    br[NL - k] = r;
+  }
+  uint64_t T = 0;
+  BGV_UNROLL for (int i = NL - 1; i >= 0; --i) T += (uint64_t)a.v[i] * br[i];
+  // t = T mod R in lanes 50..63 (0 elsewhere)
+  uint32_t t;
+  {
+    const uint64_t h = T >> LBITS;
+    const uint64_t v1 = (uint64_t)((uint32_t)T & LMASK) +
+                        (((uint64_t)wfp_shr1((uint32_t)(h >> 32), lane) << 32) | wfp_shr1((uint32_t)h, lane));
+    t = ((uint32_t)v1 & LMASK) + wfp_shr1((uint32_t)(v1 >> LBITS), lane);
+    t = low ? t : 0u;
+  }
+  const uint32_t NP[NL] = BGV_NPRIME_LIMBS;
+  uint64_t M = (uint64_t)NP[0] * t;
+  uint32_t tr = t;
+  BGV_UNROLL for (int j = 1; j < NL; ++j) {
+    tr = wfp_ror1(tr);
+    M += (uint64_t)NP[j] * tr;
+  }
+  uint32_t m;
+  {
+    const uint64_t h = M >> LBITS;
+    const uint64_t v1 = (uint64_t)((uint32_t)M & LMASK) +
+                        (((uint64_t)wfp_shr1((uint32_t)(h >> 32), lane) << 32) | wfp_shr1((uint32_t)h, lane));
+    m = ((uint32_t)v1 & LMASK) + wfp_shr1((uint32_t)(v1 >> LBITS), lane);
+    m = low ? m : 0u;
+  }
+  uint32_t mr = m;
+  T += (uint64_t)p_limb(0) * mr;
+  BGV_UNROLL for (int j = 1; j < NL; ++j) {
+    mr = wfp_ror1(mr);
+    T += (uint64_t)p_limb(j) * mr;
+  }
+  const uint64_t h = T >> LBITS;
+  const uint64_t v1 = (uint64_t)((uint32_t)T & LMASK) + (((uint64_t)wfp_ror1((uint32_t)(h >> 32)) << 32) | wfp_ror1((uint32_t)h));
+  const uint32_t v2 = ((uint32_t)v1 & LMASK) + wfp_ror1((uint32_t)(v1 >> LBITS));
+  const uint64_t lowbits = __ballot(v2 != 0) & 0xFFFC000000000000ull;
+  const uint32_t res = v2 + (lane == 0 && lowbits != 0 ? 1u : 0u);
+  return wfp_to(res);
+}
+
 #ifndef BGV_WFP_K
 #define BGV_WFP_K 2
 #endif

@@ -50,6 +50,9 @@ __global__ void __launch_bounds__(64) k_check(uint32_t* bad, uint32_t seed) {
   const fp_t q4 = wfp_to(wfp_mul_t<4, 4>(wa, wa, c)), q7 = wfp_to(wfp_mul_t<7, 2>(wa, wa, c));
   const fp_t q14 = wfp_to(wfp_mul_t<14, 2>(wa, wa, c)), q3 = wfp_to(wfp_mul3(wa, wa, c));
   const fp_t m3 = wfp_to(wfp_mul3(wa, wb, c));
+  const fp_t mu = wfp_umul(a, b), qu = wfp_umul(a, a);
+  fp_t su = a;
+  for (int k = 0; k < 8; ++k) su = wfp_umul(su, b);
   uint32_t w3 = wa;
   for (int k = 0; k < 8; ++k) w3 = wfp_mul3(w3, wb, c);
   const fp_t m0 = fp_mul_body(a, b), q0 = fp_sqr_body(a);
@@ -63,10 +66,13 @@ __global__ void __launch_bounds__(64) k_check(uint32_t* bad, uint32_t seed) {
   const fp_t d0 = fp_sub(fp_canon(m), fp_canon(m0)), d1 = fp_sub(fp_canon(q), fp_canon(q0));
   const fp_t d2 = fp_sub(fp_canon(wfp_to(w)), fp_canon(s));
   const fp_t d3 = fp_sub(fp_canon(m3), fp_canon(m0)), d4 = fp_sub(fp_canon(wfp_to(w3)), fp_canon(s));
+  const fp_t d5 = fp_sub(fp_canon(mu), fp_canon(m0)), d6 = fp_sub(fp_canon(qu), fp_canon(q0));
+  const fp_t d7 = fp_sub(fp_canon(su), fp_canon(s));
   const fp_t cq = fp_canon(q);
   const bool vok = fp_is_zero(fp_sub(fp_canon(q4), cq)) && fp_is_zero(fp_sub(fp_canon(q7), cq)) &&
                    fp_is_zero(fp_sub(fp_canon(q14), cq)) && fp_is_zero(fp_sub(fp_canon(q3), cq));
-  if (!vok || !fp_is_zero(d0) || !fp_is_zero(d1) || !fp_is_zero(d2) || !fp_is_zero(d3) || !fp_is_zero(d4)) {
+  if (!vok || !fp_is_zero(d0) || !fp_is_zero(d1) || !fp_is_zero(d2) || !fp_is_zero(d3) || !fp_is_zero(d4) ||
+      !fp_is_zero(d5) || !fp_is_zero(d6) || !fp_is_zero(d7)) {
     if (wfp_lane() == 0) atomicAdd(bad, 1u);
   }
 }
@@ -98,6 +104,12 @@ __global__ void __launch_bounds__(64) k_sqr_lane(fp_t* io, int reps) {
   fp_t x = io[blockIdx.x];
   for (int r = 0; r < reps; ++r) x = fp_sqr(x);
   io[blockIdx.x] = x;
+}
+
+__global__ void __launch_bounds__(64) k_sqr_umul(fp_t* io, int reps) {
+  fp_t x = io[blockIdx.x];
+  for (int r = 0; r < reps; ++r) x = wfp_umul(x, x);
+  if (wfp_lane() == 0) io[blockIdx.x] = x;
 }
 
 __global__ void __launch_bounds__(64) k_sqr_wave3(fp_t* io, int reps) {
@@ -179,6 +191,8 @@ int main() {
 #define SWEEP(K, A)                                                                                    \
   printf("{\"sqr_ns_wave\": %.1f, \"K\": %d, \"ACC\": %d}\n",                                           \
          time_ms([&] { hipLaunchKernelGGL((k_sqr_wave<K, A>), dim3(1), dim3(64), 0, 0, io, sq); }) * 1e6 / sq, K, A)
+  printf("{\"sqr_ns_umul\": %.1f}\n",
+         time_ms([&] { hipLaunchKernelGGL(k_sqr_umul, dim3(1), dim3(64), 0, 0, io, sq); }) * 1e6 / sq);
   printf("{\"sqr_ns_wave3\": %.1f}\n",
          time_ms([&] { hipLaunchKernelGGL(k_sqr_wave3, dim3(1), dim3(64), 0, 0, io, sq); }) * 1e6 / sq);
   SWEEP(1, 1);
