@@ -70,9 +70,9 @@ extern "C" {
 // than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane reads the same slot).
 __device__ __forceinline__ void pk_aggw_body(const bgv_dslot* __restrict__ slots, uint32_t s,
                                              const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                             g1_jac* __restrict__ pk_agg) {
+                                             g1_jac* __restrict__ pk_agg, uint32_t min_keys = BGV_PK_TEAM_MAX + 1) {
   const bgv_dslot& d = slots[s];
-  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk <= BGV_PK_TEAM_MAX) return;
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < min_keys) return;
   const uint32_t l = threadIdx.x;
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
@@ -121,25 +121,14 @@ __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slo
   if (blockIdx.x < nslots) pk_aggw_body(slots, blockIdx.x, pk_idx, cache, pk_agg);
 }
 
-// merged (the smallest calls, with k_prep_a_wave and k_prep_wide): only planes 3 and 4 run
-// here -- plane 3 sums committee-sized sets' cached keys (k_pk_agg16's teams), plane 4 larger
-// sets' (k_pk_agg's wave tree) -- and k_prep_wide does the pubkey task after them.
-// Otherwise planes 0..2 are the maps and the decoding, one lane per set, plane 3 the pubkey task.
+// The latency path's first launch for calls above BGV_PREP_WIDE_MAX sets (the smallest calls
+// run k_prep_a_wave, bgv_k_prep_wave.hip): planes 0..2 the maps of u0 / u1 and the signature's
+// decoding, one lane per set, plane 3 the pubkey task.
 __global__ void BGV_KATTR_PREP k_prep_a(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ h,
                                         fp12_t* __restrict__ f, int32_t* __restrict__ sig_status,
                                         const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                         const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                        int32_t* __restrict__ pk_status, g1_jac* __restrict__ pk_agg, int merged) {
-  if (merged && blockIdx.y >= 3) {  // block-uniform
-    if (!pk_agg) return;
-    if (blockIdx.y == 3) {
-      if (blockIdx.x < (nslots + 3) / 4) pk_agg16_body(slots, nslots, blockIdx.x, pk_idx, cache, pk_agg);
-    } else if (blockIdx.x < nslots) {
-      pk_aggw_body(slots, blockIdx.x, pk_idx, cache, pk_agg);
-    }
-    return;
-  }
-  if (merged) return;  // planes 0..2 ran in k_prep_a_wave (bgv_k_prep_wave.hip)
+                                        int32_t* __restrict__ pk_status, g1_jac* __restrict__ pk_agg) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nslots) return;
   if (blockIdx.y == 0)
@@ -244,14 +233,17 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
                                                   const uint32_t* __restrict__ pk_idx,
                                                   const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
                                                   g1_jac* __restrict__ rpk, int32_t* __restrict__ pk_status,
-                                                  const g1_jac* __restrict__ pk_agg) {
+                                                  g1_jac* __restrict__ pk_agg) {
   __shared__ uint8_t prog[TCP_TABLE_BYTES];
   __shared__ fp_t S[TCP_NSLOT];
   __shared__ fp_t RP[64];
   __shared__ int flag;
-  if (blockIdx.y == 3) {  // the pubkey task of the merged k_prep_a, one lane per set
-    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
-    if (s < nslots) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+  if (blockIdx.y == 3) {  // the pubkey task, one set per block
+    // a set of >= BGV_PK_TREE_MIN cached keys first sums them on the whole wave (k_pk_agg's
+    // tree), concurrently with the point programs of the other planes; then lane 0 runs the task
+    const uint32_t s = blockIdx.x;
+    if (pk_agg) pk_aggw_body(slots, s, pk_idx, cache, pk_agg, BGV_PK_TREE_MIN);
+    if (threadIdx.x == 0) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
     return;
   }
   const uint32_t uu = blockIdx.x;  // grid = exactly nslots blocks per task
@@ -367,9 +359,6 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
     const g1_aff* cache = reinterpret_cast<const g1_aff*>(b.cache_opaque);
     const hipError_t e = bgv_launch_prep_wave(b, s.main);
     if (e != hipSuccess) return e;
-    if (tree)  // the pubkey trees (planes 3, 4; planes 0..2 exit at once)
-      hipLaunchKernelGGL(k_prep_a, dim3(n, 5), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status, b.pk_idx,
-                         cache, b.pk_bytes, b.rpk, b.pk_status, b.pk_agg, 1);
     hipLaunchKernelGGL(k_prep_wide, dim3(n, 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
                        b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
     BGV_MARK(1);
@@ -384,7 +373,7 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
   if (bgv_use_latency(b, n + b.ngroups)) {
     hipLaunchKernelGGL(k_prep_a, dim3(nblk(n, 64), 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.sig_status,
                        b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk, b.pk_status,
-                       tree ? b.pk_agg : nullptr, 0);
+                       tree ? b.pk_agg : nullptr);
     hipLaunchKernelGGL(k_prep_team, dim3(nblk(n, BGV_FINAL_TEAMS), 3), dim3(64), 0, s.main, b.slots, n, b.h, b.f,
                        b.rsig, b.sig_status);
   } else {
