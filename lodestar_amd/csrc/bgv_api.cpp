@@ -349,9 +349,20 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // both its jobs are invalid (for b in D, S_b and its complement each hold an invalid job, and
 // every invalid job is a candidate of that one pair); a failing single job is invalid; jobs of
 // a failing pair next to other failures are tested alone in one more round.
+//
+// Weighted test (kind 2, one-set jobs, bulk rounds): before any pattern test, ONE device group
+// over the whole unit in which slot k enters with weight k + 1 (bgv_layout.h
+// BGV_GROUP_WEIGHTED): its value is W = prod_k X_k^(k+1) against the first-pass value
+// V = prod_k X_k (X_k the slot's pairing value, 1 when valid).  With exactly one invalid slot k,
+// W = V^(k+1) and the closing finds w = k + 1 (the only w <= 64 with V^w = W: V has prime order
+// r); the invalid job is identified with one test instead of ceil(log2 n).  Two or more invalid
+// jobs match no w except with probability ~2^-50 over the randomizers (the same order as a
+// pattern test passing by accident); the unit then takes the pattern tests next round
+// (unit_rounds -1).  A failing group usually holds one invalid job (at 1 % corrupted sets, 72 %
+// of the failing 64-set groups), so most are resolved with one Miller loop and one closing.
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
-  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs
+  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs; 2: weighted test
   std::vector<size_t> jobs;        // kind 0: its jobs in slot order
   std::vector<uint32_t> tests;     // round group index of each test
   std::vector<std::vector<size_t>> test_jobs;  // kind 1: each test's jobs
@@ -380,7 +391,7 @@ struct Call {
   std::vector<int32_t> set_sig, set_pk;
   std::vector<std::vector<size_t>> units;  // pending retry units
   std::vector<int> unit_group;             // first-pass group the unit's jobs lie in (-1: not known)
-  std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through
+  std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through (-1: a weighted test)
   std::vector<std::vector<uint32_t>> unit_idx;  // after a pattern round: the candidates' pattern indices
   std::vector<uint32_t> unit_dmask;        // ... and the index bits D of their pairing (0: none)
   std::vector<Part> parts;
@@ -827,17 +838,51 @@ static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int
   return true;
 }
 
+// BGV_WEIGHTED=0 turns the weighted tests off (A/B)
+static bool weighted_env() {
+  static const bool v = [] {
+    const char* e = getenv("BGV_WEIGHTED");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // Group testing for one retry round: split every pending unit into parts.  gb: the call's
 // first group in the batch when the first pass's u values are on the device (pattern tests
-// possible), else -1.
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb) {
+// possible), else -1.  weighted: the round's closing supports weighted tests (k_final12).
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb, bool weighted) {
   call->parts.clear();
   call->punits.clear();
   for (size_t ui = 0; ui < call->units.size(); ++ui) {
     const auto& u = call->units[ui];
     const int ug = call->unit_group[ui], urounds = call->unit_rounds[ui];
     const bool in_group = unit_in_group(call, u, ug);
-    if (gb >= 0 && in_group && urounds == 0 && u.size() >= 2 && pattern_eligible(call, ui)) {
+    const bool eligible = gb >= 0 && in_group && (urounds == 0 || urounds == -1) && u.size() >= 2 &&
+                          pattern_eligible(call, ui);
+    bool single_sets = true;
+    for (size_t j : u) single_sets = single_sets && call->jobs[j].n_sets == 1;
+    if (eligible && weighted && urounds == 0 && single_sets) {
+      PatternUnit pu;
+      pu.group = (uint32_t)ug;
+      pu.kind = 2;
+      const bgv_dgroup& g = call->L.groups[pu.group];
+      uint64_t m = 0;
+      for (size_t j : u) {
+        pu.jobs.push_back(j);
+        m |= job_mask(call, j, g);
+      }
+      Part part;
+      part.jobs = u;
+      part.groups.push_back((uint32_t)rg.size());
+      part.pattern = (int)call->punits.size();
+      pu.tests.push_back((uint32_t)rg.size());
+      rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1),
+                              BGV_GROUP_WEIGHTED});
+      call->parts.push_back(std::move(part));
+      call->punits.push_back(std::move(pu));
+      continue;
+    }
+    if (eligible) {
       PatternUnit pu;
       pu.group = (uint32_t)ug;
       const bgv_dgroup& g = call->L.groups[pu.group];
@@ -966,6 +1011,27 @@ static void call_after_round(Call* call, const int32_t* rv) {
     }
   }
   for (const PatternUnit& pu : call->punits) {
+    if (pu.kind == 2) {  // weighted test (see PatternUnit): the identified job, or pattern tests next
+      const int32_t v = rv[pu.tests[0]];
+      const uint32_t w = ((uint32_t)v >> 8) & 0xff;
+      const bgv_dgroup& g = call->L.groups[pu.group];
+      size_t bad = SIZE_MAX;
+      if (!(v & 1) && w >= 1)
+        for (size_t j : pu.jobs)
+          if (call->L.job_first_slot[j] == g.first_slot + (w - 1)) bad = j;
+      if (trace_on()) fprintf(stderr, "[bgv]   weighted unit: %zu jobs, w %u%s\n", pu.jobs.size(), w,
+                              bad == SIZE_MAX ? " (pattern tests next)" : "");
+      if (bad != SIZE_MAX) {
+        for (size_t j : pu.jobs) call->code[j] = j == bad ? 0 : 1;
+      } else {
+        call->units.push_back(pu.jobs);
+        call->unit_group.push_back((int)pu.group);
+        call->unit_rounds.push_back(-1);
+        call->unit_idx.emplace_back();
+        call->unit_dmask.push_back(0);
+      }
+      continue;
+    }
     if (pu.kind == 1) {  // pairs and single jobs (see PatternUnit)
       std::vector<size_t> failing;
       for (size_t t = 0; t < pu.tests.size(); ++t)
@@ -1217,6 +1283,8 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
   int rc;
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
+  // weighted tests need k_final12's closing: rounds over more slots than the latency path takes
+  const bool weighted = weighted_env() && nslots > bgv_fold_pairs_max();
   // retry rounds over the per-slot results on the device
   for (;;) {
     const auto th = std::chrono::steady_clock::now();
@@ -1224,7 +1292,7 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     std::vector<uint32_t> base;
     for (size_t k = 0; k < calls.size(); ++k) {
       base.push_back((uint32_t)rg.size());
-      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1);
+      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1, weighted);
     }
     if (rg.empty()) break;
     ++rounds;

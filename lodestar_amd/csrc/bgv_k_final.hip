@@ -86,8 +86,11 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   // present ones only (a retry test masks half of a group or a single job), the teams of the
   // wave to the longest list, multiplying by 1 past their own
   uint64_t m = live ? g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1)) : 0;
-  if (c == 0) lens[team] = (uint32_t)__popcll(m);
-  __syncthreads();
+  const bool wt = live && (g.flags & BGV_GROUP_WEIGHTED);
+  if (c == 0) lens[team] = wt ? g.n_slots : (uint32_t)__popcll(m);
+  // a wave holding a weighted test runs every team through the weighted loop's shape (two
+  // products per step, the identification below), the others' extra products by 1
+  const bool anyw = __syncthreads_or(wt ? 1 : 0) != 0;
   uint32_t nmax = 0;
   BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
   const int fi = tm_fp_index(c);
@@ -102,16 +105,58 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
     m &= m - 1;
     return fs[kFp12 * k + fi];
   };
-  fp_t y = next();
-  BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-    const fp_t yn = next();  // next operand in flight
-    x = o.mul(x, y);
-    y = yn;
+  if (!anyw) {
+    fp_t y = next();
+    BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
+      const fp_t yn = next();  // next operand in flight
+      x = o.mul(x, y);
+      y = yn;
+    }
+  } else {
+    // weighted teams: positions k = n_slots - 1 .. 0, S = prod_{k' >= k} f_k' (1 where absent),
+    // x = gpair * prod_k S_k = gpair * prod_k f_k^(k+1); the others: x = x * (next present)
+    const uint64_t mw = m;
+    uint32_t kk = wt ? g.n_slots : 0;
+    fp_t S = one_c;
+    BGV_NO_UNROLL for (uint32_t step = 0; step < nmax; ++step) {
+      fp_t y;
+      if (wt) {
+        y = one_c;
+        if (kk > 0) {
+          --kk;
+          if ((mw >> kk) & 1) y = fs[kFp12 * kk + fi];
+        }
+      } else {
+        y = next();
+      }
+      const fp_t r1 = o.mul(wt ? S : x, y);
+      const fp_t r2 = o.mul(wt ? x : one_c, wt ? r1 : one_c);
+      if (wt) {
+        S = r1;
+        x = r2;
+      } else {
+        x = r1;
+      }
+    }
   }
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const int32_t v = verdict_bits(o, u, g, gu1, fi);
+  int32_t v = verdict_bits(o, u, g, gu1, fi);
+  if (anyw && gu1) {
+    // identification: the first w with (value of ref1 - 1)^w == this value, i.e. u_ref^w conj(u)
+    // in Fp6 (values conj(u) / u); P = u_ref^w
+    const fp_t ur = wt && g.ref1 ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : one_c;
+    const fp_t cu = o.conj(u);
+    fp_t P = ur;
+    int32_t found = 0;
+    BGV_NO_UNROLL for (uint32_t w = 1; w <= nmax; ++w) {
+      const bool hit = o.is_fp6(o.mul(P, cu));
+      if (wt && g.ref1 && hit && found == 0 && w <= g.n_slots) found = (int32_t)w;
+      P = o.mul(P, ur);
+    }
+    if (wt) v = (v & 1) | (found << 8);
+  }
   if (live && c == 0) verdict[gi] = v;
 }
 
@@ -231,6 +276,8 @@ __global__ void k_fp12_from_bytes(const uint8_t* __restrict__ in, uint32_t n, fp
 // Group closing over b.groups (contiguous slot ranges of <= 64 slots) after
 // bgv_launch_miller (first pass, group pairs already made) or, for a retry round over the
 // same per-slot results, with pairs = true: the parts' signature sums and pairs first.
+uint32_t bgv_fold_pairs_max() { return bgv_latency_max(); }
+
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs) {
   if (b.ngroups == 0) return hipSuccess;
   BGV_MARK(4);

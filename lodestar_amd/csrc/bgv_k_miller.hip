@@ -61,11 +61,34 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
   g2_jac acc = jac_infinity<fp2_t>();
-  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
-    if (!grp_has(g, k)) continue;
-    const uint32_t s = g.first_slot + k;
-    const int32_t ss = sig_status[s];
-    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+  if (!(g.flags & BGV_GROUP_WEIGHTED)) {
+    for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+      if (!grp_has(g, k)) continue;
+      const uint32_t s = g.first_slot + k;
+      const int32_t ss = sig_status[s];
+      if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+    }
+  } else {
+    // sum_k (k + 1) R_k over this lane's slots k = c + 16 j: (c + 1) A + 16 B with A = sum_j R,
+    // B = sum_j j R (suffix sums, j descending); the butterfly below adds the lanes up
+    g2_jac A = jac_infinity<fp2_t>(), B = jac_infinity<fp2_t>();
+    for (int j = 3; j >= 0; --j) {
+      const uint32_t k = (uint32_t)c + BGV_TEAM * (uint32_t)j;
+      if (grp_has(g, k)) {
+        const uint32_t s = g.first_slot + k;
+        const int32_t ss = sig_status[s];
+        if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) A = jac_add(A, rsig[s]);
+      }
+      if (j >= 1) B = jac_add(B, A);
+    }
+    BGV_NO_UNROLL for (int t = 0; t < 4; ++t) B = jac_dbl(B);
+    const uint32_t w = (uint32_t)c + 1;
+    g2_jac T = jac_infinity<fp2_t>();
+    BGV_NO_UNROLL for (int bit = 4; bit >= 0; --bit) {
+      T = jac_dbl(T);
+      if ((w >> bit) & 1) T = jac_add(T, A);
+    }
+    acc = jac_add(T, B);
   }
   acc = jac_add(acc, point_xor<8>(acc));
   acc = jac_add(acc, point_xor<4>(acc));

@@ -88,6 +88,9 @@ uint32_t bgv_lines_pairs(const bgv_dev_batch& b);  // line records the batch nee
 bool bgv_single_pass_miller();                     // BGV_MILLER_1PASS: k_miller instead (A/B)
 size_t bgv_line_record_bytes();                    // bytes of one pair's 68 records
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
+// bgv_launch_groups closes with k_final12 (which takes BGV_GROUP_WEIGHTED tests) iff
+// nslots + ngroups exceeds this (else k_final_fold)
+uint32_t bgv_fold_pairs_max();
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
 size_t bgv_slot_bytes();
 size_t bgv_slot_mem_bytes(uint32_t cap_slots);  // the per-slot arrays of an Exec of cap_slots slots

@@ -180,3 +180,35 @@ def test_split_epoch_sweep_2p20(split_ctxs):
     packed = native.PackedSingleSets(b"".join(roots), bytes(broken), idx)
     want = -native.BLST_BAD_ENCODING
     assert [one.verify_packed_one_job(packed), two.verify_packed_one_job(packed)] == [want, want]
+
+
+# ---------------------------------------------------------------------------------------
+# Weighted retry tests (bgv_api.cpp PatternUnit kind 2, bgv_layout.h BGV_GROUP_WEIGHTED): a
+# failing 64-set group of one-set jobs first takes ONE test whose slot k enters with weight
+# k + 1; a single invalid job is identified from W == V^(k+1), several fall through to the
+# pattern tests.  Only rounds over more slots than BGV_LATENCY_MAX (16,384) use it, so the
+# call here holds 20,480 jobs.  Reference semantics: every job's verdict equals its own
+# verification (chain/bls/multithread/worker.ts:76-98 retry per job).
+# ---------------------------------------------------------------------------------------
+def test_weighted_retry_large_call(split_ctxs):
+    from lodestar_amd import native
+    (one, _), sks = split_ctxs
+    n = 20480
+    idx, roots, sigs = _sweep_sets(one, sks, n, 0x20480)
+    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[idx[i]]) for i in range(n)]
+    want = [1] * n
+    # one invalid job per group at offsets 0, 1, 37, 63; two in one group; three in one group;
+    # an undecodable signature beside one invalid job
+    wrong = [64 * 3 + 0, 64 * 10 + 1, 64 * 50 + 37, 64 * 99 + 63, 64 * 120 + 3, 64 * 120 + 40,
+             64 * 200 + 5, 64 * 200 + 6, 64 * 200 + 62, 64 * 319 + 17]
+    for i in wrong:
+        sets[i] = native.SetSpec(roots[(i + 128) % n], sets[i].sig, pk_indices=[idx[i]])
+        want[i] = 0
+    bad = 64 * 300 + 9
+    sets[bad] = native.SetSpec(roots[bad], bytes([sets[bad].sig[0] & 0x7F]) + sets[bad].sig[1:], pk_indices=[idx[bad]])
+    want[bad] = -native.BLST_BAD_ENCODING
+    sets[64 * 300 + 30] = native.SetSpec(roots[0], sets[64 * 300 + 30].sig, pk_indices=[idx[64 * 300 + 30]])
+    want[64 * 300 + 30] = 0
+    st = native.BgvStats()
+    got = one.verify_jobs([([s], True) for s in sets], native.MODE_WORKER, stats=st)
+    assert got == want
