@@ -70,9 +70,9 @@ extern "C" {
 // than BGV_PK_TREE_MIN cached keys exit at once (uniformly: every lane reads the same slot).
 __device__ __forceinline__ void pk_aggw_body(const bgv_dslot* __restrict__ slots, uint32_t s,
                                              const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                             g1_jac* __restrict__ pk_agg, uint32_t min_keys = BGV_PK_TEAM_MAX + 1) {
+                                             g1_jac* __restrict__ pk_agg) {
   const bgv_dslot& d = slots[s];
-  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < min_keys) return;
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk <= BGV_PK_TEAM_MAX) return;
   const uint32_t l = threadIdx.x;
   g1_jac acc = jac_infinity<fp_t>();
   for (uint32_t k = l; k < d.n_pk; k += 64) acc = jac_add_aff(acc, cache[pk_idx[d.pk_off + k]]);
@@ -113,6 +113,31 @@ __device__ __forceinline__ void pk_agg16_body(const bgv_dslot* __restrict__ slot
   acc = jac_add(acc, point_xor<2>(acc));
   acc = jac_add(acc, point_xor<1>(acc));
   if (act && l == 0) pk_agg[s] = acc;
+}
+
+// One set's tree sum on a whole 64-lane block with the bulk path's summation order (so the
+// same Jacobian representative, hence the same Miller value f): k_pk_agg16's 16-lane team for
+// BGV_PK_TREE_MIN..BGV_PK_TEAM_MAX cached keys (lanes 16..63 repeat lanes 0..15), k_pk_agg's
+// wave tree above.
+__device__ __forceinline__ void pk_agg_one(const bgv_dslot* __restrict__ slots, uint32_t s,
+                                           const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                           g1_jac* __restrict__ pk_agg) {
+  const bgv_dslot& d = slots[s];
+  if ((d.flags & BGV_SLOT_PAD) || !(d.flags & BGV_SLOT_PK_CACHED) || d.n_pk < BGV_PK_TREE_MIN) return;
+  if (d.n_pk > BGV_PK_TEAM_MAX) {
+    pk_aggw_body(slots, s, pk_idx, cache, pk_agg);
+    return;
+  }
+  const uint32_t l = threadIdx.x % 16;
+  const uint32_t* idx = pk_idx + d.pk_off;
+  const uint32_t n = d.n_pk;
+  g1_jac acc = jac_from_aff(cache[idx[l]]);
+  for (uint32_t k = l + 16; k < n; k += 16) acc = jac_add_aff(acc, cache[idx[k]]);
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (threadIdx.x == 0) pk_agg[s] = acc;
 }
 
 __global__ void __launch_bounds__(64) k_pk_agg(const bgv_dslot* __restrict__ slots, uint32_t nslots,
@@ -242,7 +267,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
     // a set of >= BGV_PK_TREE_MIN cached keys first sums them on the whole wave (k_pk_agg's
     // tree), concurrently with the point programs of the other planes; then lane 0 runs the task
     const uint32_t s = blockIdx.x;
-    if (pk_agg) pk_aggw_body(slots, s, pk_idx, cache, pk_agg, BGV_PK_TREE_MIN);
+    if (pk_agg) pk_agg_one(slots, s, pk_idx, cache, pk_agg);
     if (threadIdx.x == 0) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
     return;
   }

@@ -194,7 +194,10 @@ __device__ __forceinline__ uint32_t wfp_mul3(uint32_t a, uint32_t b, const wfp_c
 // rotated; t N' and m p take N' and p as scalar constants and rotate t and m instead (lane L
 // reads lane L - j: wave_ror steps; t and m are masked to lanes 50..63, so terms outside a
 // column's range read 0).  The value equals fp_mul_body's: (ab + mp) / R with m = -ab/p mod R.
-__device__ __noinline__ fp_t wfp_umul(const fp_t a, const fp_t b) {
+// (limbs as 28 scalar arguments, as fp_mul_l: a second struct argument would travel through
+// scratch memory on every call)
+__device__ __noinline__ fp_t wfp_umul_l(BGV_U14(a_), BGV_U14(b_)) {
+  const fp_t a = {{BGV_L14(a_)}}, b = {{BGV_L14(b_)}};
   const uint32_t lane = wfp_lane();
   const bool low = lane >= 50;
   uint32_t r = 0;
@@ -243,6 +246,7 @@ __device__ __noinline__ fp_t wfp_umul(const fp_t a, const fp_t b) {
   const uint32_t res = v2 + (lane == 0 && lowbits != 0 ? 1u : 0u);
   return wfp_to(res);
 }
+__device__ __forceinline__ fp_t wfp_umul(const fp_t& a, const fp_t& b) { return wfp_umul_l(BGV_V14(a), BGV_V14(b)); }
 
 #ifndef BGV_WFP_K
 #define BGV_WFP_K 2

@@ -294,9 +294,9 @@ __device__ __forceinline__ fp_t fp_sqr(const fp_t& a) {
 #elif defined(__HIP_DEVICE_COMPILE__) && defined(BGV_WAVE_UNIFORM_MUL)
 // BGV_WAVE_UNIFORM_MUL (device code of a unit whose kernels run one set per wave, every lane
 // holding the same values): each product on the whole wave (bgv_wfp.h wfp_umul, defined there).
-__device__ __noinline__ fp_t wfp_umul(const fp_t a, const fp_t b);
-__device__ __forceinline__ fp_t fp_mul(const fp_t& a, const fp_t& b) { return wfp_umul(a, b); }
-__device__ __forceinline__ fp_t fp_sqr(const fp_t& a) { return wfp_umul(a, a); }
+__device__ __noinline__ fp_t wfp_umul_l(BGV_U14(a_), BGV_U14(b_));
+__device__ __forceinline__ fp_t fp_mul(const fp_t& a, const fp_t& b) { return wfp_umul_l(BGV_V14(a), BGV_V14(b)); }
+__device__ __forceinline__ fp_t fp_sqr(const fp_t& a) { return wfp_umul_l(BGV_V14(a), BGV_V14(a)); }
 #else
 BGV_HD fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_mul_l(BGV_V14(a), BGV_V14(b)); }
 BGV_HD fp_t fp_sqr(const fp_t& a) { return fp_sqr_l(BGV_V14(a)); }
