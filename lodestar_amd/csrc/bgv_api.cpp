@@ -435,6 +435,10 @@ struct bgv_ctx {
   // BGV_FAULT_INJECT=1 at bgv_init: every super-batch fails as a HIP error would (tests of
   // the device-error path: every job in flight rejects with BGV_E_DEVICE, none resolves false)
   bool fault_inject = false;
+  // BGV_WEIGHTED=1 at bgv_init: retry rounds start a failing group of one-set jobs with a
+  // weighted test (PatternUnit kind 2).  Off by default: it saves tests but adds a retry round,
+  // and at 1 % corrupted sets the bench measured 2.08 M vs 2.40 M sets/s (profiles/r04/weighted_ab/).
+  bool weighted = false;
   // super-batch geometry (bgv_set_batching; env defaults at bgv_init)
   std::atomic<uint32_t> max_slots{BGV_MAX_BATCH_SLOTS};
   std::atomic<uint32_t> coalesce{BGV_COALESCE_US};
@@ -836,15 +840,6 @@ static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int
     if (jg.size() != 1 || jg[0] != (uint32_t)g) return false;
   }
   return true;
-}
-
-// BGV_WEIGHTED=0 turns the weighted tests off (A/B)
-static bool weighted_env() {
-  static const bool v = [] {
-    const char* e = getenv("BGV_WEIGHTED");
-    return !(e && *e == '0');
-  }();
-  return v;
 }
 
 // Group testing for one retry round: split every pending unit into parts.  gb: the call's
@@ -1284,7 +1279,7 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
   // weighted tests need k_final12's closing: rounds over more slots than the latency path takes
-  const bool weighted = weighted_env() && nslots > bgv_fold_pairs_max();
+  const bool weighted = c->weighted && nslots > bgv_fold_pairs_max();
   // retry rounds over the per-slot results on the device
   for (;;) {
     const auto th = std::chrono::steady_clock::now();
@@ -1513,6 +1508,8 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   {
     const char* fi = getenv("BGV_FAULT_INJECT");
     c->fault_inject = fi && atoi(fi) > 0;
+    const char* we = getenv("BGV_WEIGHTED");
+    c->weighted = we && atoi(we) > 0;
   }
   c->max_slots = (uint32_t)max_batch_slots();
   c->coalesce = (uint32_t)coalesce_us();

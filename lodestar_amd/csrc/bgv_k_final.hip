@@ -120,9 +120,10 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
     fp_t S = one_c;
     BGV_NO_UNROLL for (uint32_t step = 0; step < nmax; ++step) {
       fp_t y;
+      const bool more = kk > 0;  // a weighted team past its last position multiplies by 1
       if (wt) {
         y = one_c;
-        if (kk > 0) {
+        if (more) {
           --kk;
           if ((mw >> kk) & 1) y = fs[kFp12 * kk + fi];
         }
@@ -130,7 +131,7 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
         y = next();
       }
       const fp_t r1 = o.mul(wt ? S : x, y);
-      const fp_t r2 = o.mul(wt ? x : one_c, wt ? r1 : one_c);
+      const fp_t r2 = o.mul(wt ? x : one_c, wt && more ? r1 : one_c);
       if (wt) {
         S = r1;
         x = r2;

@@ -5,7 +5,9 @@
 // of ~490 on one lane) and the square roots' exponentiations stay in the limb-per-lane form
 // (bgv_pow_wave).  Planes (blockIdx.y): 0 / 1 the SSWU map + isogeny of u0 / u1, 2 the
 // signature's decoding; the same tasks and formulas as k_prep_a's lane planes (bgv_k_lat.h).
+#ifndef BGV_PREP_WAVE_LANE_MUL  // A/B: the other products on one lane's schedule (bgv_pow_wave only)
 #define BGV_WAVE_UNIFORM_MUL 1
+#endif
 #include "bgv_k_lat.h"
 #include "bgv_wfp.h"
 

@@ -190,25 +190,52 @@ def test_split_epoch_sweep_2p20(split_ctxs):
 # call here holds 20,480 jobs.  Reference semantics: every job's verdict equals its own
 # verification (chain/bls/multithread/worker.ts:76-98 retry per job).
 # ---------------------------------------------------------------------------------------
-def test_weighted_retry_large_call(split_ctxs):
+@pytest.fixture(scope="module")
+def weighted_ctx():
+    """A context with the weighted retry tests on (BGV_WEIGHTED=1 is read at bgv_init)."""
+    import os
     from lodestar_amd import native
-    (one, _), sks = split_ctxs
     n = 20480
-    idx, roots, sigs = _sweep_sets(one, sks, n, 0x20480)
-    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[idx[i]]) for i in range(n)]
+    sks = [_interop_sk(i) for i in range(n)]
+    old = os.environ.get("BGV_WEIGHTED")
+    os.environ["BGV_WEIGHTED"] = "1"
+    try:
+        c = native.Context([0])
+    finally:
+        if old is None:
+            del os.environ["BGV_WEIGHTED"]
+        else:
+            os.environ["BGV_WEIGHTED"] = old
+    c.keygen(b"".join(sks), cache_first=0, want_pubkeys=False)
+    yield c, sks
+    c.close()
+
+
+def test_weighted_retry_large_call(weighted_ctx):
+    import hashlib
+    from lodestar_amd import native
+    c, sks = weighted_ctx
+    n = 20480
+    roots = [hashlib.sha256(b"weighted-%d" % (i // 128)).digest() for i in range(n)]
+    sigs = c.sign(b"".join(sks), b"".join(roots))
+    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[i]) for i in range(n)]
     want = [1] * n
     # one invalid job per group at offsets 0, 1, 37, 63; two in one group; three in one group;
     # an undecodable signature beside one invalid job
     wrong = [64 * 3 + 0, 64 * 10 + 1, 64 * 50 + 37, 64 * 99 + 63, 64 * 120 + 3, 64 * 120 + 40,
              64 * 200 + 5, 64 * 200 + 6, 64 * 200 + 62, 64 * 319 + 17]
     for i in wrong:
-        sets[i] = native.SetSpec(roots[(i + 128) % n], sets[i].sig, pk_indices=[idx[i]])
+        sets[i] = native.SetSpec(roots[(i + 128) % n], sets[i].sig, pk_indices=[i])
         want[i] = 0
     bad = 64 * 300 + 9
-    sets[bad] = native.SetSpec(roots[bad], bytes([sets[bad].sig[0] & 0x7F]) + sets[bad].sig[1:], pk_indices=[idx[bad]])
+    sets[bad] = native.SetSpec(roots[bad], bytes([sets[bad].sig[0] & 0x7F]) + sets[bad].sig[1:], pk_indices=[bad])
     want[bad] = -native.BLST_BAD_ENCODING
-    sets[64 * 300 + 30] = native.SetSpec(roots[0], sets[64 * 300 + 30].sig, pk_indices=[idx[64 * 300 + 30]])
+    sets[64 * 300 + 30] = native.SetSpec(roots[0], sets[64 * 300 + 30].sig, pk_indices=[64 * 300 + 30])
     want[64 * 300 + 30] = 0
     st = native.BgvStats()
-    got = one.verify_jobs([([s], True) for s in sets], native.MODE_WORKER, stats=st)
+    got = c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER, stats=st)
     assert got == want
+    # 320 first-pass groups, 8 failing: one weighted test each; the six single-invalid groups
+    # are resolved there, the two- and three-invalid groups take 2 x 6 pattern tests and then
+    # pairs / single jobs.  Without identifications it would be >= 320 + 8 + 8 x 6.
+    assert st.device_groups < 320 + 8 + 8 * 6, st.device_groups
