@@ -109,6 +109,14 @@ static int execs_per_device() {
   return std::max(v, dispatchers_per_device());
 }
 
+// Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
+// retry rounds of several super-batches then run side by side instead of queueing behind one
+// another (their rounds are latency-bound chains of small launches)
+static int retry_threads_per_device() {
+  static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
+  return v;
+}
+
 extern "C" int bgv_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -216,8 +224,8 @@ struct DevSched {
   std::deque<Exec*> free;
   std::deque<RetryJob> rq;
   bool stop = false;
-  std::thread retry_thread;
-  hipStream_t retry = nullptr;
+  std::vector<std::thread> retry_threads;
+  std::vector<hipStream_t> retries;  // one stream per retry thread
   std::vector<hipStream_t> dstreams;
 };
 
@@ -1370,7 +1378,7 @@ static void finish_calls(std::vector<Call*>& calls, int rc) {
 
 // The device's retry thread: the retry rounds of handed-over super-batches, in order; drains
 // the queue before it stops.
-static void retry_loop(bgv_ctx* c, Device* d) {
+static void retry_loop(bgv_ctx* c, Device* d, int k) {
   DevSched& s = *d->sched;
   (void)hipSetDevice(d->id);
   for (;;) {
@@ -1382,7 +1390,7 @@ static void retry_loop(bgv_ctx* c, Device* d) {
       job = std::move(s.rq.front());
       s.rq.pop_front();
     }
-    job.x->close = s.retry;
+    job.x->close = s.retries[k];
     // No cache_mu here: the retry kernels (k_gsum, the group pairs, the closing) read only the
     // per-slot results of pass 1 (r_i sig_i, f_i, u values), never the pubkey cache, and
     // bgv_close joins this thread before it frees the devices.  A batch in its retry rounds
@@ -1482,8 +1490,8 @@ static void ctx_free_devices(bgv_ctx* c) {
     d.sched->free.clear();
     for (hipStream_t st : d.sched->dstreams) (void)hipStreamDestroy(st);
     d.sched->dstreams.clear();
-    if (d.sched->retry) (void)hipStreamDestroy(d.sched->retry);
-    d.sched->retry = nullptr;
+    for (hipStream_t st : d.sched->retries) (void)hipStreamDestroy(st);
+    d.sched->retries.clear();
     if (d.stream) (void)hipStreamSynchronize(d.stream);
     if (d.cache) (void)hipFree(d.cache);
     d.cache = nullptr;
@@ -1523,8 +1531,12 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
     bool ok = d.id >= 0 && d.id < avail && hipSetDevice(d.id) == hipSuccess &&
               hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
     int least = 0, greatest = 0;
-    ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-         hipStreamCreateWithPriority(&d.sched->retry, hipStreamNonBlocking, greatest) == hipSuccess;
+    ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+    for (int k = 0; ok && k < retry_threads_per_device(); ++k) {
+      hipStream_t st = nullptr;
+      ok = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest) == hipSuccess;
+      if (ok) d.sched->retries.push_back(st);
+    }
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
       hipStream_t st = nullptr;
       ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
@@ -1545,7 +1557,7 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   }
   for (Device& d : c->devs) {
     for (hipStream_t st : d.sched->dstreams) c->dispatchers.emplace_back(dispatcher_loop, c, &d, st);
-    d.sched->retry_thread = std::thread(retry_loop, c, &d);
+    for (int k = 0; k < (int)d.sched->retries.size(); ++k) d.sched->retry_threads.emplace_back(retry_loop, c, &d, k);
   }
   *out = c;
   return BGV_OK;
@@ -1573,7 +1585,9 @@ int bgv_close(bgv_ctx* c) {
       d.sched->stop = true;
     }
     d.sched->cv.notify_all();
-    if (d.sched->retry_thread.joinable()) d.sched->retry_thread.join();
+    for (auto& t : d.sched->retry_threads)
+      if (t.joinable()) t.join();
+    d.sched->retry_threads.clear();
   }
   std::unique_lock<std::shared_mutex> lk(c->cache_mu);
   if (c->closed.exchange(true)) return BGV_OK;
