@@ -129,16 +129,36 @@ int main() {
     std::vector<fp_t> a(6 * nb), b(6 * nb);
     CHECK(hipMemcpy(a.data(), d4, sizeof(fp_t) * a.size(), hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(b.data(), dw, sizeof(fp_t) * b.size(), hipMemcpyDeviceToHost));
-    int bad = 0, first = -1;
-    for (size_t i = 0; i < a.size(); ++i)
+    // equal as field elements: both engines leave weakly reduced values (< 2p), whose
+    // representatives may differ by p (the four-part engine reduces a sum of four parts)
+    auto plus_p = [](const fp_t& x) {
+      fp_t r;
+      uint32_t c = 0;
+      for (int l = 0; l < NL; ++l) {
+        const uint32_t t = x.v[l] + p_limb(l) + c;
+        r.v[l] = l < NL - 1 ? (t & LMASK) : t;
+        c = t >> LBITS;
+      }
+      return r;
+    };
+    auto same = [](const fp_t& x, const fp_t& y) {
       for (int l = 0; l < NL; ++l)
-        if (a[i].v[l] != b[i].v[l]) {
-          if (first < 0) first = (int)i;
-          ++bad;
-          break;
-        }
-    printf("{\"check\": \"wave4 vs four-part engine\", \"mode\": %d, \"fp_values\": %zu, \"mismatches\": %d, \"first\": %d}\n",
-           mode, a.size(), bad, first);
+        if (x.v[l] != y.v[l]) return false;
+      return true;
+    };
+    int bad = 0, first = -1, plus = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+      if (same(a[i], b[i])) continue;
+      if (same(plus_p(a[i]), b[i]) || same(plus_p(b[i]), a[i])) {
+        ++plus;
+        continue;
+      }
+      if (first < 0) first = (int)i;
+      ++bad;
+    }
+    printf("{\"check\": \"wave4 vs four-part engine (mod p)\", \"mode\": %d, \"fp_values\": %zu, \"mismatches\": %d, "
+           "\"representatives_differing_by_p\": %d, \"first\": %d}\n",
+           mode, a.size(), bad, plus, first);
     if (bad) {
       printf("{\"a0\": [");
       for (int l = 0; l < NL; ++l) printf("%u%s", a[first].v[l], l + 1 < NL ? "," : "");
