@@ -167,12 +167,23 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
 // chain).  The final exponentiation then runs on the
 // whole block with each coefficient's products split over eight lanes (tm_wide_ops_t<false, 8>):
 // one double-width product per lane for a squaring (two for a product) instead of 7 on one.
+// LEAN: the squarings with the lane's operand recipes (bgv_team_dev.h tm_wide8_lean_ops; the
+// same parts bit for bit); BGV_FOLD_LEAN=0 selects the select-based forms for an A/B.
+}  // extern "C"
+template <bool LEAN>
+__device__ auto bgv_fold_ops_pick() {
+  if constexpr (LEAN)
+    return tm_wide8_lean_ops{};
+  else
+    return tm_wide_ops_t<false, 8>{};
+}
 #define BGV_FOLD_TEAMS 8  // 16-lane teams of k_final_fold's 128-thread block
-__global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
-                                       const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
-                                       int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
-                                       fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
-                                       const fp12_t* __restrict__ fsig) {
+template <bool LEAN>
+__device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                                const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
+                                                int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
+                                                fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
+                                                const fp12_t* __restrict__ fsig) {
   __shared__ fp_t lds[BGV_FOLD_TEAMS][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FOLD_TEAMS][BGV_TEAM_COMPS];
   __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[8 * BGV_TEAM_COMPS];
@@ -209,13 +220,31 @@ __global__ void __launch_bounds__(128) k_final_fold(const bgv_dgroup* __restrict
   if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
   __syncthreads();
   const int wc = threadIdx.x % BGV_TEAM_COMPS, wq = threadIdx.x / BGV_TEAM_COMPS;
-  tm_wide_ops_t<false, 8> ow{WA, WB, WP, wc, wq};
+  using OW = decltype(bgv_fold_ops_pick<LEAN>());
+  OW ow;
+  ow.A = WA;
+  ow.B = WB;
+  ow.P = WP;
+  ow.c = wc;
+  ow.q = wq;
+  if constexpr (LEAN) tm_sqr_rec8(wc, wq, &ow.rx, &ow.ry);
   const fp_t xw = W[wc];
   const int wfi = tm_fp_index(wc);
   const fp_t u = tm_final_exp_u(ow, xw);
   if (gu && gi < ngroups && wq == 0) reinterpret_cast<fp_t*>(gu + gi)[wfi] = u;
   const int32_t v = verdict_bits(ow, u, g, gu1, wfi);
   if (gi < ngroups && threadIdx.x == 0) verdict[gi] = v;
+}
+extern "C" {
+#define BGV_FOLD_ARGS                                                                                         \
+  const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const fp12_t *__restrict__ f,                     \
+      const fp12_t *__restrict__ gpair, int32_t *__restrict__ verdict, fp12_t *__restrict__ gprod,          \
+      fp12_t *__restrict__ gu, const fp12_t *__restrict__ gu1, const fp12_t *__restrict__ fsig
+__global__ void __launch_bounds__(128) k_final_fold(BGV_FOLD_ARGS) {
+  final_fold_body<true>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+}
+__global__ void __launch_bounds__(128) k_final_fold_sel(BGV_FOLD_ARGS) {
+  final_fold_body<false>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
 }
 
 // Products of runs of Fp12 values (cross-process partials): team t of the
@@ -286,8 +315,13 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     const hipError_t e = bgv_launch_gpairs(b, s.main);
     if (e != hipSuccess) return e;
   }
+  static const bool lean = [] {
+    const char* e = getenv("BGV_FOLD_LEAN");
+    return !(e && atoi(e) == 0);
+  }();
   if (b.nslots + b.ngroups <= bgv_latency_max())
-    hipLaunchKernelGGL(k_final_fold, dim3(b.ngroups), dim3(128), 0, s.main, b.groups, b.ngroups, b.f, b.gpair,
+    hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(128), 0, s.main, b.groups,
+                       b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,
                        !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
   else

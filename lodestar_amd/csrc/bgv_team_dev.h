@@ -146,3 +146,16 @@ struct tm_wide_ops_t {
   }
 };
 using tm_wide_ops = tm_wide_ops_t<false>;
+
+// Eight-part ops with the lean squaring (bls_team.h tm_sqr_rec8): the lane's two operand
+// recipes are fixed once, a squaring evaluates only them.  Same parts, bit for bit.
+struct tm_wide8_lean_ops : tm_wide_ops_t<false, 8> {
+  tm_lin_t rx, ry;
+  __device__ fp_t sqr(const fp_t& x) {
+    if (q == 0) A[c] = x;
+    sync();
+    if (q < 8) P[q * BGV_TEAM_COMPS + c] = tm_sqr_part8_lean(A, rx, ry);
+    sync();
+    return gather();
+  }
+};

@@ -280,6 +280,70 @@ BGV_HD fp_t tm_sqr_part8(int c, int q, const fp_t* A) {
   return wide_redc(t);
 }
 
+// Lean operands for the eight-part squaring.  A lane of k_final_fold keeps its (c, q) for the
+// whole final exponentiation, and tm_sqr_part8 needs ONE X and ONE Y of the many it computes
+// and selects between (d, s, 2p - x1, doubled forms, the diagonal's sums).  Each is an exact
+// integer u1 S[i1] + u2 S[i2] + k p (|u| <= 2, k p keeping it >= 0), so a lane can evaluate
+// just its own from a recipe fixed at kernel start: one 14-limb signed chain per operand.
+// The integers are those tm_sqr_part8 forms, carry-normalized the same way, so the products
+// and parts are bit-identical (tests/test_hostsim_math.py).
+struct tm_lin_t {
+  int i1, i2, u1, u2, k;
+};
+
+// Components have limbs < 2^28 below the top one and values < 2p: every limb sum
+// u1 a + u2 b + k p_l + carry stays within 2^31, so the chain runs in 32-bit signed arithmetic.
+BGV_HD fp_t tm_lin(const fp_t* S, const tm_lin_t& r) {
+  const fp_t a = S[r.i1], b = S[r.i2];
+  const uint32_t P_[NL] = BGV_P_LIMBS;
+  fp_t o;
+  int32_t cy = 0;
+  BGV_UNROLL for (int l = 0; l < NL - 1; ++l) {
+    const int32_t s = r.u1 * (int32_t)a.v[l] + r.u2 * (int32_t)b.v[l] + r.k * (int32_t)P_[l] + cy;
+    o.v[l] = (uint32_t)s & LMASK;
+    cy = s >> LBITS;
+  }
+  o.v[NL - 1] = (uint32_t)(r.u1 * (int32_t)a.v[NL - 1] + r.u2 * (int32_t)b.v[NL - 1] + r.k * (int32_t)P_[NL - 1] + cy);
+  return o;
+}
+
+// the recipes of tm_sqr_part8's operands for lane (c, q)
+BGV_HD void tm_sqr_rec8(int c, int q, tm_lin_t* X, tm_lin_t* Y) {
+  const int k = c >> 1, e = c & 1;
+  const uint32_t kI[6] = {0x321, 0x320, 0x430, 0x410, 0x510, 0x210};
+  const uint32_t kJ[6] = {0x345, 0x451, 0x452, 0x523, 0x534, 0x345};
+  const uint32_t kW[6] = {0x7, 0x6, 0x6, 0x4, 0x4, 0x0};
+  if (q < 6) {
+    const int p = q >> 1;
+    const int i = (kI[k] >> (4 * p)) & 0xf, j = (kJ[k] >> (4 * p)) & 0xf;
+    const bool wrap = (kW[k] >> p) & 1, cross = i != j;
+    const tm_lin_t y0 = {2 * j, 2 * j, 1, 0, 0}, y1 = {2 * j + 1, 2 * j + 1, 1, 0, 0};
+    const tm_lin_t d = {2 * j, 2 * j + 1, 1, -1, 2}, s = {2 * j, 2 * j + 1, 1, 1, 0};
+    const int m = cross ? 2 : 1;  // a cross pair's x operand doubled (fp_select(c, a, b) = c ? b : a)
+    if ((q & 1) == 0) {
+      *X = {2 * i, 2 * i, m, 0, 0};
+      *Y = wrap ? (e ? s : d) : (e ? y1 : y0);
+    } else {
+      *X = e ? tm_lin_t{2 * i + 1, 2 * i + 1, m, 0, 0} : tm_lin_t{2 * i + 1, 2 * i + 1, -m, 0, 2 * m};
+      *Y = wrap ? (e ? d : s) : (e ? y0 : y1);
+    }
+  } else if (q == 6 && (k & 1) == 0) {  // the unwrapped diagonal of even k
+    const int h = k >> 1;
+    *X = e ? tm_lin_t{2 * h, 2 * h, 2, 0, 0} : tm_lin_t{2 * h, 2 * h + 1, 1, 1, 0};
+    *Y = e ? tm_lin_t{2 * h + 1, 2 * h + 1, 1, 0, 0} : tm_lin_t{2 * h, 2 * h + 1, 1, -1, 2};
+  } else {  // a zero product
+    *X = {0, 0, 0, 0, 0};
+    *Y = {0, 0, 1, 0, 0};
+  }
+}
+
+BGV_HD fp_t tm_sqr_part8_lean(const fp_t* A, const tm_lin_t& X, const tm_lin_t& Y) {
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  wide_mac(t, tm_lin(A, X), tm_lin(A, Y));
+  return wide_redc(t);
+}
+
 BGV_HD fp_t tm_mul_line_part8(int c, int q, const fp_t* A, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
   const int k = c >> 1, e = c & 1;
   uint64_t t[2 * NL];
@@ -551,6 +615,17 @@ struct tm_emu_wide8_ops : tm_emu_ops {
   }
   BGV_HD tm_emu_t mul_line(const tm_emu_t& a, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
     return gather8([&](int c, int q) { return tm_mul_line_part8(c, q, a.c, l0, l1, l3); });
+  }
+};
+
+// the same with the lean squaring (tm_sqr_rec8 / tm_sqr_part8_lean)
+struct tm_emu_wide8_lean_ops : tm_emu_wide8_ops {
+  BGV_HD tm_emu_t sqr(const tm_emu_t& a) {
+    return gather8([&](int c, int q) {
+      tm_lin_t X, Y;
+      tm_sqr_rec8(c, q, &X, &Y);
+      return tm_sqr_part8_lean(a.c, X, Y);
+    });
   }
 };
 

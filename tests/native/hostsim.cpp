@@ -280,6 +280,32 @@ int hs_team_final_is_one_wide8(const uint8_t* f) {
   tm_emu_wide8_ops o;
   return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
 }
+// the lean eight-part squaring (k_final_fold): value and, part by part, the raw limbs of
+// tm_sqr_part8 (returns the number of (c, q) parts that differ)
+void hs_team_sqr_wide8_lean(uint8_t* r, const uint8_t* a) {
+  tm_emu_wide8_lean_ops o;
+  out_fp12(r, tm_emu_to_fp12(o.sqr(tm_emu_from_fp12(in_fp12(a)))));
+}
+int hs_team_sqr8_lean_diff(const uint8_t* a) {
+  const tm_emu_t x = tm_emu_from_fp12(in_fp12(a));
+  int bad = 0;
+  for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+    for (int q = 0; q < 8; ++q) {
+      tm_lin_t X, Y;
+      tm_sqr_rec8(c, q, &X, &Y);
+      const fp_t u = tm_sqr_part8(c, q, x.c), v = tm_sqr_part8_lean(x.c, X, Y);
+      for (int l = 0; l < NL; ++l)
+        if (u.v[l] != v.v[l]) {
+          ++bad;
+          break;
+        }
+    }
+  return bad;
+}
+int hs_team_final_is_one_wide8_lean(const uint8_t* f) {
+  tm_emu_wide8_lean_ops o;
+  return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));
+}
 // Q handed over in Jacobian form with Z != 1: (l^2 x, l^3 y, l), l = 3 + 5u
 static g2_jac jac_scaled(const g2_aff& a) {
   const fp2_t l = {fp_to_mont(fp_t{{3}}), fp_to_mont(fp_t{{5}})};

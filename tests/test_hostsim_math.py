@@ -399,6 +399,9 @@ def test_team_fp12_ops(L):
         assert got.raw == want.raw
         L.hs_team_sqr_wide8(got, a)
         assert got.raw == want.raw
+        L.hs_team_sqr_wide8_lean(got, a)  # operand recipes per lane (k_final_fold)
+        assert got.raw == want.raw
+        assert L.hs_team_sqr8_lean_diff(a) == 0  # the same 96 parts, limb for limb
         for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
             tf(got, a)
             ref(want, a)
@@ -416,6 +419,7 @@ def test_team_final_exp_check(L):
         assert L.hs_team_final_is_one(f) == 0
         assert L.hs_team_final_is_one_wide(f) == 0
         assert L.hs_team_final_is_one_wide8(f) == 0
+        assert L.hs_team_final_is_one_wide8_lean(f) == 0
     p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
     q = g2_rand_in_group()
     # e(P, Q) e(-P, Q) == 1 and e(P, Q) e(-P, Q2) != 1 (Miller values multiplied)
@@ -427,6 +431,7 @@ def test_team_final_exp_check(L):
     assert L.hs_team_final_is_one(m.raw) == 1
     assert L.hs_team_final_is_one_wide(m.raw) == 1
     assert L.hs_team_final_is_one_wide8(m.raw) == 1
+    assert L.hs_team_final_is_one_wide8_lean(m.raw) == 1
     q2 = g2_rand_in_group()
     L.hs_miller_loop(b, hs.g1_b(o.g1_neg(p)), hs.g2_b(q2))
     L.hs_fp12_mul(m, a.raw, b.raw)
@@ -434,3 +439,4 @@ def test_team_final_exp_check(L):
     assert L.hs_team_final_is_one(m.raw) == 0
     assert L.hs_team_final_is_one_wide(m.raw) == 0
     assert L.hs_team_final_is_one_wide8(m.raw) == 0
+    assert L.hs_team_final_is_one_wide8_lean(m.raw) == 0
