@@ -51,7 +51,7 @@ struct tc_dev_engine {
   __device__ void check_add() {
     if (c == 0) {
       const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
-      bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+      bad = bad || z2(TC_CHK_A) || z2(TC_CHK_B);
     }
   }
 };
@@ -244,7 +244,7 @@ struct tc_wide_engine : tr_wide_engine {
   __device__ void check_add() {
     if (q == 0 && c == 0) {
       const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
-      bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+      bad = bad || z2(TC_CHK_A) || z2(TC_CHK_B);
     }
   }
 };
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
       S[TCP_BANK(4) + c] = v;
     }
     __syncthreads();
-    const int a = tc_mul_x_abs(e);
+    const int a = tc_to_jac(e, tc_mul_x_abs(e));
     if (lane == 0) {
       const g2_jac p = jac_from_aff(*split_sig(f, uu));
       bool in;
@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(256) k_prep_wide4(const bgv_dslot* __restrict_
       S[TCP_BANK(4) + t] = v;
     }
     __syncthreads();
-    const int a = tc_mul_x_abs(e);
+    const int a = tc_to_jac(e, tc_mul_x_abs(e));
     if (t == 0) {
       const g2_jac p = jac_from_aff(*split_sig(f, uu));
       bool in;

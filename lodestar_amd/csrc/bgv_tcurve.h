@@ -2,15 +2,17 @@
 // and r_i * sig_i on a team of 16 lanes (one set per team), from the generated point
 // programs of bgv_tcurve_prog.h (tools/gen_tcurve.py; the round model of bgv_tmiller.h).
 //
-// A doubling is 3 rounds and an addition 5, against ~16 and ~43 chained products on one
-// lane, so the two 64-bit [x]-chains of the cofactor clearing and the 2-bit-window r * sig
-// (tc_mul_glv) finish ~2x sooner on an otherwise idle chip.  The schedules below restate bls_curve.h
+// The chains run in homogeneous projective coordinates (tools/gen_tcurve.py): a doubling is
+// 2 rounds and an addition 3 (Jacobian: 3 and 5), against ~16 and ~43 chained products on one
+// lane.  Every schedule converts its input banks from Jacobian and its result back (j2p /
+// p2j programs), so callers hand in and take out Jacobian points as before: the same points
+// as bls_curve.h's formulas give, other representatives.  The schedules below restate bls_curve.h
 // step by step (g2_clear_cofactor, jac_mul_u64) over point "banks" of six LDS slots; the
 // engine E supplies the program runs and the bank moves, so the same schedule runs on the
 // device (bgv_k_prep.hip) and in the host emulation (tests/native/hostsim.cpp).
 //
 // The additions are the generic-case formulas.  tc_clear_cofactor flags an addition whose
-// inputs coincide or include infinity (H, Z1 or Z2 zero) and the caller then recomputes
+// inputs share x or include infinity (v^2 or Z1 Z2 zero) and the caller then recomputes
 // with the complete one-lane formulas; for hash outputs this never happens in practice.
 // In tc_mul_u64 the only exceptional addition is the first (accumulator at infinity), which
 // the schedule handles by selecting the table entry instead.
@@ -18,19 +20,28 @@
 #include "bgv_tmiller.h"
 #include "bgv_tcurve_prog.h"
 
-#define TC_HH TCP_S_HH
-#define TC_Z1Z1 (TCP_S_HH - 18)  // the add programs' first two temporaries (gen_tcurve.py)
-#define TC_Z2Z2 (TCP_S_HH - 16)
+// the addition programs' exceptional-case witnesses: v^2 and Z1 Z2 (tools/gen_tcurve.py)
+#define TC_CHK_A TCP_S_VV
+#define TC_CHK_B TCP_S_ZZ
 
-// [|x|]P: base in bank 0, accumulator (= P) in bank 4 on entry; returns the result's bank
+// the projective point in bank b -> Jacobian in bank 1 (returns 1)
+template <class E>
+BGV_HD int tc_to_jac(E& e, int b) {
+  e.copy(3, b);
+  e.run(TCP_P2J31);
+  return 1;
+}
+
+// [|x|]P, projective: base in bank 0, accumulator (= P) in bank 4 on entry; returns the
+// result's bank
 template <class E>
 BGV_HD int tc_mul_x_abs(E& e) {
   int acc = 4;
   for (int i = 62; i >= 0; --i) {
-    e.run(acc == 4 ? TCP_DBL45 : TCP_DBL54);
+    e.run(acc == 4 ? TCP_PDBL45 : TCP_PDBL54);
     acc = 9 - acc;
     if ((BGV_X_ABS >> i) & 1) {
-      e.run(acc == 4 ? TCP_ADD405 : TCP_ADD504);
+      e.run(acc == 4 ? TCP_PADD405 : TCP_PADD504);
       e.check_add();
       acc = 9 - acc;
     }
@@ -39,10 +50,14 @@ BGV_HD int tc_mul_x_abs(E& e) {
 }
 
 // RFC 9380 G.4 (bls_curve.h g2_clear_cofactor) of q0 + q1: q0 in bank 1, q1 in bank 2 on
-// entry, the result in bank 3.  Storage banks: 6 = P, 7 = t1, 8 = t2, 9 = t3.
+// entry (Jacobian), the result in bank 3 (Jacobian).  Storage banks: 6 = P, 7 = t1, 8 = t2,
+// 9 = t3.
 template <class E>
 BGV_HD void tc_clear_cofactor(E& e) {
-  e.run(TCP_ADD123);  // P = q0 + q1
+  e.run(TCP_J2P12_45);  // q0, q1 -> projective
+  e.copy(1, 4);
+  e.copy(2, 5);
+  e.run(TCP_PADD123);  // P = q0 + q1
   e.check_add();
   e.copy(6, 3);
   e.copy(0, 3);
@@ -54,19 +69,19 @@ BGV_HD void tc_clear_cofactor(E& e) {
   e.run(TCP_PSI12);
   e.copy(8, 2);
   e.copy(4, 6);  // t3 = psi2(2P)
-  e.run(TCP_DBL45);
+  e.run(TCP_PDBL45);
   e.copy(1, 5);
   e.run(TCP_PSI2_12);
   e.copy(9, 2);
   e.copy(1, 9);  // t3 = t3 - t2
   e.copy(2, 8);
   e.neg_y(2);
-  e.run(TCP_ADD123);
+  e.run(TCP_PADD123);
   e.check_add();
   e.copy(9, 3);
   e.copy(1, 7);  // t2 = [x](t1 + t2)
   e.copy(2, 8);
-  e.run(TCP_ADD123);
+  e.run(TCP_PADD123);
   e.check_add();
   e.copy(0, 3);
   e.copy(4, 3);
@@ -75,47 +90,51 @@ BGV_HD void tc_clear_cofactor(E& e) {
   e.copy(8, a);
   e.copy(1, 9);  // t3 = t3 + t2
   e.copy(2, 8);
-  e.run(TCP_ADD123);
+  e.run(TCP_PADD123);
   e.check_add();
   e.copy(9, 3);
   e.copy(1, 9);  // t3 = t3 - t1
   e.copy(2, 7);
   e.neg_y(2);
-  e.run(TCP_ADD123);
+  e.run(TCP_PADD123);
   e.check_add();
   e.copy(9, 3);
   e.copy(1, 9);  // t3 - P
   e.copy(2, 6);
   e.neg_y(2);
-  e.run(TCP_ADD123);
+  e.run(TCP_PADD123);
   e.check_add();
+  tc_to_jac(e, 3);
+  e.copy(3, 1);
 }
 
 // [k]P for the team's 64-bit k (bls_curve.h jac_mul_u64: 2-bit fixed window over the table
-// P, 2P, 3P): P in bank 1 on entry, the result in bank 4.  Every window runs the same
+// P, 2P, 3P): P in bank 1 on entry, the result in bank 4 (both Jacobian).  Every window runs the same
 // programs on every team (lane-uniform control flow); the per-team digit only picks bank
 // sources: table entry d -> bank 0, and the new accumulator from bank 4 (d = 0), bank 5
 // (acc + entry) or bank 0 (accumulator still at infinity).
 template <class E>
 BGV_HD void tc_mul_u64(E& e, uint64_t k) {
-  e.copy(4, 1);
-  e.run(TCP_DBL45);
-  e.copy(2, 5);       // 2P
-  e.run(TCP_ADD123);  // 3P
+  e.run(TCP_J2P12_45);
+  e.copy(1, 4);
+  e.run(TCP_PDBL45);
+  e.copy(2, 5);        // 2P
+  e.run(TCP_PADD123);  // 3P
   bool inf = true;
   for (int i = 62; i >= 0; i -= 2) {
-    e.run(TCP_DBL45);
-    e.run(TCP_DBL54);
+    e.run(TCP_PDBL45);
+    e.run(TCP_PDBL54);
     const int d = (int)((k >> i) & 3u);
     e.copy(0, d ? d : 1);
-    e.run(TCP_ADD405);
+    e.run(TCP_PADD405);
     e.copy(4, d == 0 ? 4 : (inf ? 0 : 5));
     inf = inf && d == 0;
   }
+  e.copy(4, tc_to_jac(e, 4));
 }
 
 // r P for the randomizer r = lo32(k) + hi32(k) x^2 (bls_curve.h jac_mul_glv) with 2-bit
-// windows: P in bank 1 on entry, the result in bank 4.  Tables: P, 2P, 3P in banks 1-3 and
+// windows: P in bank 1 on entry, the result in bank 4 (both Jacobian).  Tables: P, 2P, 3P in banks 1-3 and
 // psi^2 of them (= [x^2] times, P in G2) in banks 6-8.  Per window: two doublings, then the
 // a-digit's and the b-digit's entries added through bank 0 (the per-team digit picks the
 // source bank), the accumulator taking the entry itself while it is still at infinity.
@@ -124,11 +143,12 @@ BGV_HD void tc_mul_u64(E& e, uint64_t k) {
 template <class E>
 BGV_HD void tc_mul_glv(E& e, uint64_t k) {
   const uint32_t a = (uint32_t)k, b = (uint32_t)(k >> 32);
+  e.run(TCP_J2P12_45);
+  e.copy(1, 4);
   e.copy(0, 1);  // P
-  e.copy(4, 1);
-  e.run(TCP_DBL45);
-  e.copy(2, 5);       // 2P
-  e.run(TCP_ADD123);  // 3P
+  e.run(TCP_PDBL45);
+  e.copy(2, 5);        // 2P
+  e.run(TCP_PADD123);  // 3P
   e.copy(9, 2);
   e.run(TCP_PSI2_12);  // bank 1 still P
   e.copy(6, 2);
@@ -142,19 +162,20 @@ BGV_HD void tc_mul_glv(E& e, uint64_t k) {
   e.copy(2, 9);
   bool inf = true;
   for (int i = 30; i >= 0; i -= 2) {
-    e.run(TCP_DBL45);
-    e.run(TCP_DBL54);
+    e.run(TCP_PDBL45);
+    e.run(TCP_PDBL54);
     const int da = (int)((a >> i) & 3u);
     e.copy(0, da ? da : 1);
-    e.run(TCP_ADD405);
+    e.run(TCP_PADD405);
     e.copy(4, da == 0 ? 4 : (inf ? 0 : 5));
     inf = inf && da == 0;
     const int db = (int)((b >> i) & 3u);
     e.copy(0, db ? 5 + db : 6);
-    e.run(TCP_ADD405);
+    e.run(TCP_PADD405);
     e.copy(4, db == 0 ? 4 : (inf ? 0 : 5));
     inf = inf && db == 0;
   }
+  e.copy(4, tc_to_jac(e, 4));
 }
 
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -174,7 +195,7 @@ struct tc_host_engine {
   }
   void check_add() {
     const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
-    bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+    bad = bad || z2(TC_CHK_A) || z2(TC_CHK_B);
   }
 };
 

@@ -206,7 +206,7 @@ struct tc_wave4_engine {
   __device__ void check_add() {
     if (threadIdx.x == 0) {
       const auto z2 = [&](int s) { return fp_is_zero(S[s]) && fp_is_zero(S[s + 1]); };
-      bad = bad || z2(TC_HH) || z2(TC_Z1Z1) || z2(TC_Z2Z2);
+      bad = bad || z2(TC_CHK_A) || z2(TC_CHK_B);
     }
   }
 };

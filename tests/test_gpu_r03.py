@@ -73,6 +73,14 @@ def _mixed_sets(ctx):
     return sets
 
 
+def _pairing(f576):
+    """final_exp of a device Miller value on the host (tests/native/hostsim.cpp)"""
+    from tests import hostsim as hs
+    out = hs.buf(576)
+    hs.lib().hs_final_exp(out, f576)
+    return out.raw
+
+
 def test_latency_vs_bulk_miller_values(ctx):
     from lodestar_amd import native
     sets = _mixed_sets(ctx)
@@ -83,7 +91,9 @@ def test_latency_vs_bulk_miller_values(ctx):
         for i, (b, l) in enumerate(zip(bulk, lat)):
             assert b[2:] == l[2:], ("status", i, b[2:], l[2:])
             assert b[0] == l[0], ("H(m)", i)
-            assert b[1] == l[1], ("f", i)
+            # the latency path's G2 chains run in projective coordinates (tools/gen_tcurve.py),
+            # so f is another representative: the pairing values agree
+            assert _pairing(b[1]) == _pairing(l[1]), ("f", i)
         live = [st == 0 and pk == 0 for _, _, st, pk in bulk]
         assert live[:-2] == [True] * (len(sets) - 2) and live[-2:] == [False, False]
         assert all(f != ONE_FP12 for (_, f, _, _), lv in zip(bulk, live) if lv)
@@ -107,5 +117,11 @@ def test_latency_team_kernels_vs_bulk(ctx):
     bulk = ctx.debug_prepare(sets, native.PATH_BULK, seed=11)
     lat = ctx.debug_prepare(sets, native.PATH_LATENCY, seed=11)
     assert len(bulk) == len(lat) == 1100
+    seen = {}
     for i, (b, l) in enumerate(zip(bulk, lat)):
-        assert b == l, i
+        assert (b[0], b[2], b[3]) == (l[0], l[2], l[3]), i
+        if b[1] != l[1]:  # projective G2 chains on the latency path: compare pairing values
+            key = (b[1], l[1])
+            if key not in seen:
+                seen[key] = _pairing(b[1]) == _pairing(l[1])
+            assert seen[key], i

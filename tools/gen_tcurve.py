@@ -1,18 +1,29 @@
 """Generates lodestar_amd/csrc/bgv_tcurve_prog.h: G2 point programs for a team of 16 lanes
-(the latency path's cofactor clearing and r * sig, bgv_tcurve.h).
+(the latency path's cofactor clearing, r * sig and the subgroup check's [|x|]P, bgv_tcurve.h).
 
 Same instruction model as tools/gen_tmiller.py (one Fp output per lane per round,
 REDC(sum_k lin(A_k) lin(B_k)), bounds tracked per slot), over fixed point "banks" of six
-Fp slots (X, Y, Z as Fp2 pairs).  Programs restate bls_curve.h:
+Fp slots (X, Y, Z as Fp2 pairs).  The chains run in HOMOGENEOUS projective coordinates
+(x = X/Z, y = Y/Z), whose formulas have lower degree than the Jacobian ones, so they need
+fewer rounds (a round squares the degree at most):
 
-  dbl45 / dbl54   jac_dbl (dbl-2009-l), bank 4 -> 5 and 5 -> 4      3 rounds
-  add405 / add504 jac_add_raw (add-2007-bl), bank 4|5 + bank 0      5 rounds
-  add123          jac_add_raw, bank 1 + bank 2 -> bank 3            5 rounds
-  psi12           g2_psi: (conj(X) cx, conj(Y) cy, conj(Z)), 1 -> 2  1 round
-  psi2_12         g2_psi2: (X c, Y c', Z), 1 -> 2                     1 round
+  pdbl45 / pdbl54   doubling for y^2 = x^3 + b', b' = 4(1 + u):  U = 3b'Z^2,
+                    X3 = 2XY (Y^2 - 3U), Y3 = Y^2 (Y^2 + 6U) - 3U^2, Z3 = 8 Y^2 (YZ)     2 rounds
+                    (Jacobian dbl-2009-l: 3)
+  padd405 / padd504 / padd123   addition (add-1998-cmo-2 regrouped): R1 the cross products
+                    Y2Z1, Y1Z2, X2Z1, X1Z2, Z1Z2 (u, v linear in them); R2 u^2, v^2 and six
+                    degree-4 products; R3 X3 = u^2 (v Z1Z2) - v^2 (v^2 + 2 v X1Z2),
+                    Y3 = v^2 (3 u X1Z2 + uv - v Y1Z2) - u^2 (u Z1Z2), Z3 = v^2 (v Z1Z2)  3 rounds
+                    (Jacobian add-2007-bl: 5)
+  psi12 / psi2_12   g2_psi / g2_psi2: the same maps in either coordinates               1 round
+  j2p12_45          Jacobian banks 1, 2 -> projective banks 4, 5: (XZ, Y, Z^3)         2 rounds
+  p2j31             projective bank 3 -> Jacobian bank 1: (XZ, YZ^2, Z)                2 rounds
 
-Additions are the generic-case formulas; the driver checks H != 0 (slot TCP_S_HH of the
-add programs) and falls back to the complete one-lane formulas if it ever is.
+The schedules convert at their entry and exit, so every bank handed in or out is Jacobian,
+as bls_curve.h's one-lane formulas use (same points, other representatives).  Additions
+are the generic-case formulas; the driver checks v^2 != 0 and Z1Z2 != 0 (slots TCP_S_VV,
+TCP_S_ZZ of the addition programs) and falls back to the complete one-lane formulas if
+either ever is zero.
 
     python tools/gen_tcurve.py
 """
@@ -54,66 +65,90 @@ def bounds_with(*banks):
     return b
 
 
-def prog_dbl(src, dst):
-    g = Prog("dbl%d%d" % (src, dst), bounds_with(src))
+def mul_b3(a):
+    """3 b' a = 12 (1 + u) a as a pair of forms"""
+    return (scale(add(a[0], scale(a[1], -1)), 12), scale(add(a[0], a[1]), 12))
+
+
+def neg_prod(c, d):
+    """-(c d) as extra product terms of mul2 (re, im)"""
+    return ([(scale(c[0], -1), d[0]), (c[1], d[1])], [(scale(c[0], -1), d[1]), (scale(c[1], -1), d[0])])
+
+
+def prog_pdbl(src, dst):
+    g = Prog("pdbl%d%d" % (src, dst), bounds_with(src))
     X, Y, Z = (pair(t) for t in bank(src))
     X3o, Y3o, Z3o = bank(dst)
-    A = g.sqr2(X)
-    B = g.sqr2(Y)
-    g.mul2(lin2((2, Y)), Z, out=Z3o)  # Z3 = 2 Y Z
+    XY = g.mul2(X, Y)
+    Y2 = g.sqr2(Y)
+    YZ = g.mul2(Y, Z)
+    U = g.mul2(Z, mul_b3(Z))
     g.new_round()
-    C = g.sqr2(B)
-    G = g.sqr2(lin2((1, X), (1, B)))
-    F = g.sqr2(lin2((3, A)))
-    g.new_round()
-    # X3 = F - 2D, D = 2(G - A - C);  Y3 = E (D - X3) - 8C, E = 3A
-    g.ident2(lin2((1, F), (-4, G), (4, A), (4, C)), X3o)
-    E = lin2((3, A))
-    DmX3 = lin2((6, G), (-6, A), (-6, C), (-1, F))
-    nC8 = lin2((-8, C))
-    g.mul2(E, DmX3, out=Y3o, extra=([(nC8[0], S(ONE))], [(nC8[1], S(ONE))]))
+    g.mul2(lin2((2, XY)), lin2((1, Y2), (-3, U)), out=X3o)
+    g.mul2(Y2, lin2((1, Y2), (6, U)), out=Y3o, extra=neg_prod(lin2((3, U)), U))
+    g.mul2(lin2((8, Y2)), YZ, out=Z3o)
     return g
 
 
-HH_SLOTS = {}
+CHK_SLOTS = {}
 
 
-def prog_add(a, b, dst):
-    g = Prog("add%d%d%d" % (a, b, dst), bounds_with(a, b))
+def prog_padd(a, b, dst):
+    g = Prog("padd%d%d%d" % (a, b, dst), bounds_with(a, b))
     X1, Y1, Z1 = (pair(t) for t in bank(a))
     X2, Y2, Z2 = (pair(t) for t in bank(b))
     X3o, Y3o, Z3o = bank(dst)
-    # R1: Z1Z1, Z2Z2, Y1 Z2, Y2 Z1, Zs = (Z1 + Z2)^2 - Z1Z1 - Z2Z2 = 2 Z1 Z2
-    Z1Z1 = g.sqr2(Z1)
-    Z2Z2 = g.sqr2(Z2)
-    Y1Z2 = g.mul2(Y1, Z2)
-    Y2Z1 = g.mul2(Y2, Z1)
-    Zs = g.mul2(lin2((2, Z1)), Z2)
+    A1 = g.mul2(Y2, Z1)
+    A2 = g.mul2(Y1, Z2)
+    B1 = g.mul2(X2, Z1)
+    B2 = g.mul2(X1, Z2)
+    ZZ = g.mul2(Z1, Z2)
     g.new_round()
-    # R2: U1 = X1 Z2Z2, U2 = X2 Z1Z1, S1 = Y1 Z2 Z2Z2, S2 = Y2 Z1 Z1Z1
-    U1 = g.mul2(X1, Z2Z2)
-    U2 = g.mul2(X2, Z1Z1)
-    S1 = g.mul2(Y1Z2, Z2Z2)
-    S2 = g.mul2(Y2Z1, Z1Z1)
+    u = lin2((1, A1), (-1, A2))
+    v = lin2((1, B1), (-1, B2))
+    uu = g.sqr2(u)
+    vv = g.sqr2(v)
+    vZZ = g.mul2(v, ZZ)
+    vB2 = g.mul2(v, B2)
+    uB2 = g.mul2(u, B2)
+    uZZ = g.mul2(u, ZZ)
+    uv = g.mul2(u, v)
+    vA2 = g.mul2(v, A2)
     g.new_round()
-    # R3: H = U2 - U1, HH = H^2, r = 2(S2 - S1), rr = r^2, Z3 = Zs H
-    H = lin2((1, U2), (-1, U1))
-    r = lin2((2, S2), (-2, S1))
-    HH = g.sqr2(H)
-    rr = g.sqr2(r)
-    g.mul2(Zs, H, out=Z3o)
+    g.mul2(uu, vZZ, out=X3o, extra=neg_prod(vv, lin2((1, vv), (2, vB2))))
+    g.mul2(vv, lin2((3, uB2), (1, uv), (-1, vA2)), out=Y3o, extra=neg_prod(uu, uZZ))
+    g.mul2(vv, vZZ, out=Z3o)
+    CHK_SLOTS[g.name] = (list(vv[0])[0], list(ZZ[0])[0])
+    return g
+
+
+def prog_j2p(pairs, name):
+    """Jacobian (X, Y, Z) -> projective (X Z, Y, Z^3) for each (src, dst) bank pair"""
+    g = Prog(name, bounds_with(*[s for s, _ in pairs]))
+    zz = {}
+    for src, dst in pairs:
+        X, Y, Z = (pair(t) for t in bank(src))
+        X3o, Y3o, _ = bank(dst)
+        g.mul2(X, Z, out=X3o)
+        g.ident2(Y, Y3o)
+        zz[src] = g.sqr2(Z)
     g.new_round()
-    # R4: I = 4 HH, J = H I, V = U1 I
-    J = g.mul2(lin2((4, H)), HH)
-    V = g.mul2(lin2((4, U1)), HH)
+    for src, dst in pairs:
+        Z = pair(bank(src)[2])
+        g.mul2(Z, zz[src], out=bank(dst)[2])
+    return g
+
+
+def prog_p2j(src, dst):
+    """projective (X, Y, Z) -> Jacobian (X Z, Y Z^2, Z)"""
+    g = Prog("p2j%d%d" % (src, dst), bounds_with(src))
+    X, Y, Z = (pair(t) for t in bank(src))
+    X3o, Y3o, Z3o = bank(dst)
+    g.mul2(X, Z, out=X3o)
+    g.ident2(Z, Z3o)
+    zz = g.sqr2(Z)
     g.new_round()
-    # R5: X3 = rr - J - 2V, Y3 = r (V - X3) - 2 S1 J
-    g.ident2(lin2((1, rr), (-1, J), (-2, V)), X3o)
-    VmX3 = lin2((3, V), (-1, rr), (1, J))
-    nS1 = lin2((-2, S1))
-    g.mul2(r, VmX3, out=Y3o, extra=([(nS1[0], J[0]), (scale(S1[1], 2), J[1])],
-                                    [(nS1[0], J[1]), (nS1[1], J[0])]))
-    HH_SLOTS[g.name] = (list(HH[0])[0], list(HH[1])[0])
+    g.mul2(Y, zz, out=Y3o)
     return g
 
 
@@ -179,17 +214,18 @@ def emit(progs):
          "#define TCP_S_DUMMY %d" % DUMMY, "#define TCP_BANK(k) (%d + 6 * (k))" % BANK0]
     for name, off in offsets.items():
         L.append("#define TCP_%s %d" % (name.upper(), off))
-    hh = set(HH_SLOTS.values())
-    assert len(hh) == 1, hh  # every add program uses the same HH temporaries
-    L.append("#define TCP_S_HH %d" % list(hh)[0][0])
+    chk = set(CHK_SLOTS.values())
+    assert len(chk) == 1, chk  # every addition program uses the same v^2 / Z1Z2 temporaries
+    L.append("#define TCP_S_VV %d" % list(chk)[0][0])
+    L.append("#define TCP_S_ZZ %d" % list(chk)[0][1])
     L.append("#define TCP_TABLE_BYTES %d" % len(table))
     L.append("#define TCP_TABLE_INIT {%s}" % ",".join(str(b) for b in table))
     return "\n".join(L) + "\n"
 
 
 def main():
-    progs = [prog_dbl(4, 5), prog_dbl(5, 4), prog_add(4, 0, 5), prog_add(5, 0, 4), prog_add(1, 2, 3),
-             prog_psi(1, 2), prog_psi2(1, 2)]
+    progs = [prog_pdbl(4, 5), prog_pdbl(5, 4), prog_padd(4, 0, 5), prog_padd(5, 0, 4), prog_padd(1, 2, 3),
+             prog_psi(1, 2), prog_psi2(1, 2), prog_j2p([(1, 4), (2, 5)], "j2p12_45"), prog_p2j(3, 1)]
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lodestar_amd", "csrc",
                        "bgv_tcurve_prog.h")
     open(out, "w").write(emit(progs))
