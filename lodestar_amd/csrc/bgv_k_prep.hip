@@ -14,10 +14,12 @@
 #include "bgv_k_lat.h"
 #include "bgv_team_dev.h"
 #include "bgv_tcurve.h"
+#include "bgv_tg1.h"
 #include "bgv_tround_dev.h"
 #include "bgv_wround.h"
 
 static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
+static __constant__ uint8_t kTg1Prog[TG1_TABLE_BYTES] = TG1_TABLE_INIT;
 
 // Device engine of the team G2 schedules (bgv_tcurve.h): programs over the team's LDS slots
 // with a block barrier per round; every team of the block runs the same sequence.
@@ -249,6 +251,14 @@ struct tc_wide_engine : tr_wide_engine {
   }
 };
 
+// The G1 schedule (bgv_tg1.h) on the same four-part engine: three-slot banks.
+struct tg1_wide_engine : tr_wide_engine {
+  __device__ void copy(int dst, int src) {
+    if (q == 0 && c < 3 && dst != src) S[TG1_BANK(dst) + c] = S[TG1_BANK(src) + c];
+    __syncthreads();
+  }
+};
+
 // k_prep_team for the smallest calls, one set per 64-lane block and task (blockIdx.y): 0 the
 // cofactor clearing of q0 + q1, 1 r_i * sig_i, 2 the signature's subgroup check psi(P) ==
 // [x]P with [|x|]P from the same point programs (a team-level exceptional addition falls
@@ -260,16 +270,37 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
                                                   const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
                                                   g1_jac* __restrict__ rpk, int32_t* __restrict__ pk_status,
                                                   g1_jac* __restrict__ pk_agg) {
+  static_assert(TG1_TABLE_BYTES <= TCP_TABLE_BYTES && TG1_NSLOT <= TCP_NSLOT, "plane 3 reuses the G2 buffers");
   __shared__ uint8_t prog[TCP_TABLE_BYTES];
   __shared__ fp_t S[TCP_NSLOT];
   __shared__ fp_t RP[64];
   __shared__ int flag;
   if (blockIdx.y == 3) {  // the pubkey task, one set per block
     // a set of >= BGV_PK_TREE_MIN cached keys first sums them on the whole wave (k_pk_agg's
-    // tree), concurrently with the point programs of the other planes; then lane 0 runs the task
+    // tree); lane 0 then takes the set's sum and status, and r * sum runs on the G1 point
+    // programs (bgv_tg1.h) as rounds, concurrently with the other planes' G2 programs
     const uint32_t s = blockIdx.x;
     if (pk_agg) pk_agg_one(slots, s, pk_idx, cache, pk_agg);
-    if (threadIdx.x == 0) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
+    if (threadIdx.x == 0) {
+      g1_jac acc;
+      const bool go = task_pk_sum(s, slots, pk_idx, cache, pk_bytes, pk_status, pk_agg, &acc);
+      flag = go ? 1 : 0;
+      if (go) {
+        S[TG1_BANK(1)] = acc.x;
+        S[TG1_BANK(1) + 1] = acc.y;
+        S[TG1_BANK(1) + 2] = acc.z;
+      }
+      S[TG1_S_ONE] = fp_one();
+      S[TG1_S_BETA] = fp_t{BGV_BETA_MX2};
+    }
+    for (int i = threadIdx.x; i < TG1_TABLE_BYTES; i += 64) prog[i] = kTg1Prog[i];
+    __syncthreads();
+    if (!flag) return;  // uniform over the block
+    const int lane = threadIdx.x;
+    tg1_wide_engine e{{prog, S, RP, lane % BGV_TEAM, lane / BGV_TEAM, false}};
+    tg1_mul_glv(e, slots[s].scalar);
+    if (lane < 3) reinterpret_cast<fp_t*>(rpk + s)[lane] = S[TG1_BANK(4) + lane];
+    if (lane == 0) pk_status[s] = BGV_ST_OK;
     return;
   }
   const uint32_t uu = blockIdx.x;  // grid = exactly nslots blocks per task

@@ -77,6 +77,28 @@ __device__ __noinline__ static g1_jac pk_sum(const bgv_dslot& d, const uint32_t*
   return acc;
 }
 
+// task_pk's first half for the latency path (k_prep_wide runs r * acc on point programs,
+// bgv_tg1.h): the set's key sum into *acc and true when the multiplication remains, else the
+// final status written and false.
+static __device__ __noinline__ bool task_pk_sum(uint32_t s, const bgv_dslot* __restrict__ slots,
+                                                const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
+                                                const uint8_t* __restrict__ pk_bytes, int32_t* __restrict__ pk_status,
+                                                const g1_jac* __restrict__ pk_agg, g1_jac* acc) {
+  const bgv_dslot& d = slots[s];
+  if (d.flags & BGV_SLOT_PAD) {
+    pk_status[s] = BGV_ST_INFINITY;
+    return false;
+  }
+  int32_t st = BGV_ST_OK;
+  const g1_jac a = pk_sum(d, pk_idx, cache, pk_bytes, pk_agg, s, &st);
+  if (st != BGV_OK || jac_is_inf(a)) {  // r * acc is infinity iff acc is (acc in G1, r != 0 mod r_G1)
+    pk_status[s] = st != BGV_OK ? st : BGV_ST_INFINITY;
+    return false;
+  }
+  *acc = a;
+  return true;
+}
+
 static __device__ __noinline__ void task_pk(uint32_t s, const bgv_dslot* __restrict__ slots,
                                      const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
                                      const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,

@@ -11,6 +11,7 @@
 #include "../../lodestar_amd/csrc/bls_team.h"
 #include "../../lodestar_amd/csrc/bgv_tmiller.h"
 #include "../../lodestar_amd/csrc/bgv_tcurve.h"
+#include "../../lodestar_amd/csrc/bgv_tg1.h"
 
 static fp_t in_fp(const uint8_t* be) { return fp_to_mont(fp_from_be48(be)); }
 static void out_fp(uint8_t* be, const fp_t& a) { fp_to_be48(be, fp_from_mont(a)); }
@@ -348,6 +349,12 @@ int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
   return jac_eq(tc_mul_glv_host(h_lane, k), jac_mul_glv(h_lane, k)) ? 1 : 0;
 }
 // the latency path's team loop (bgv_tmiller.h: table-driven twist-point rounds + team Fp12)
+// the latency path's G1 schedule (bgv_tg1.h tg1_mul_glv, projective programs) against the
+// one-lane jac_mul_glv, P handed in Jacobian with Z != 1: 1 when the points agree
+int hs_tg1_check(const uint8_t* p_aff, uint64_t k) {
+  const g1_jac p = g1_scaled(in_g1(p_aff));
+  return jac_eq(tg1_mul_glv_host(p, k), jac_mul_glv(p, k)) ? 1 : 0;
+}
 void hs_tmiller(uint8_t* out, const uint8_t* p, const uint8_t* q) {
   out_fp12(out, tm_team_miller_host(g1_scaled(in_g1(p)), jac_scaled(in_g2(q))));
 }

@@ -328,6 +328,21 @@ def test_table_driven_team_miller_loop(L):
         assert tm.raw == m1.raw
 
 
+def test_team_g1_schedule(L):
+    """r * pk through the latency path's G1 point programs (bgv_tg1.h, projective, emulated
+    lane by lane, plain and as four-part instructions) equals jac_mul_glv as a point, for
+    random keys and randomizer words (full, a single low digit, a 40-bit word, a high half only)."""
+    import ctypes
+    for wide in (0, 1):
+        L.hs_set_wide_rounds(wide)
+        try:
+            for scalar in (rnd.getrandbits(64) | 1, 1, rnd.getrandbits(40) | 1, 1 << 45, (1 << 64) - 1):
+                p = o.g1_mul(o.G1, rnd.randrange(1, o.R))
+                assert L.hs_tg1_check(hs.g1_b(p), ctypes.c_uint64(scalar)) == 1, (wide, scalar)
+        finally:
+            L.hs_set_wide_rounds(0)
+
+
 def test_team_g2_schedules(L):
     """The latency path's team cofactor clearing and r * sig (bgv_tcurve.h, generated point
     programs, emulated lane by lane) equal g2_clear_cofactor and jac_mul_glv as points, for

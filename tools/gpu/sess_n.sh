@@ -1,4 +1,4 @@
-# Round-4 session n: projective point programs in the latency path (k_prep_wide chains in
+# Round-4 session n: latency-path point programs (projective G2 chains, G1 r * pk programs,
 # 2-round doublings / 3-round additions): GPU suite, config-3 latency, kernel trace, Node gossip.
 #   bash tools/gpu/sess_n.sh OUTDIR
 set -o pipefail
