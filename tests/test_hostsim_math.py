@@ -313,19 +313,24 @@ def test_miller_loop1_and_team_loop(L):
 
 
 def test_table_driven_team_miller_loop(L):
-    """The latency path's team Miller loop (bgv_tmiller.h: generated twist-point rounds,
-    tools/gen_tmiller.py, and the coefficient-parallel Fp12 accumulator), emulated lane by
-    lane, equals miller_loop1 exactly (same formulas, same line scaling) for random pairs
-    and for -G1 with a random Q."""
+    """The latency path's team Miller loop (bgv_tmiller.h: generated twist-point rounds in
+    projective coordinates, tools/gen_tmiller.py, and the coefficient-parallel Fp12
+    accumulator), emulated lane by lane, gives miller_loop1's pairing value (its lines differ
+    by Fp2 factors only) for random pairs and for -G1 with a random Q, and a different Q a
+    different value."""
+    fe = lambda m: (lambda out: (L.hs_final_exp(out, m), out.raw)[1])(hs.buf(576))
     for k in range(3):
         p = o.g1_mul(o.G1, rnd.randrange(1, o.R)) if k else o.g1_neg(o.G1)
         q = g2_rand_in_group()
         m1, tm = hs.buf(576), hs.buf(576)
         L.hs_miller_loop1(m1, hs.g1_b(p), hs.g2_b(q))
+        want = fe(m1.raw)
         L.hs_tmiller(tm, hs.g1_b(p), hs.g2_b(q))
-        assert tm.raw == m1.raw
+        assert tm.raw != m1.raw and fe(tm.raw) == want
         L.hs_tmiller_wide(tm, hs.g1_b(p), hs.g2_b(q))  # k_miller_wide: four-part instructions
-        assert tm.raw == m1.raw
+        assert fe(tm.raw) == want
+        L.hs_tmiller(tm, hs.g1_b(p), hs.g2_b(g2_rand_in_group()))
+        assert fe(tm.raw) != want
 
 
 def test_team_g1_schedule(L):

@@ -4,12 +4,19 @@ loop as a table-driven program for a team of 16 lanes.
 Every round is one instruction per lane: out = REDC(sum_k lin(A_k) * lin(B_k)), where a
 lin() is a small integer combination of LDS slots plus K * p (K makes it non-negative) and
 REDC is one Montgomery reduction of the double-width sum (bls_team.h wide_mac /
-wide_redc).  The rounds restate bls_pairing.h exactly (same formulas, same line scaling),
-so the team loop's Fp12 value equals miller_loop1's:
+wide_redc).  The twist point T runs in HOMOGENEOUS projective coordinates (x = X/Z,
+y = Y/Z; the Jacobian Q converted once), whose formulas need fewer rounds than
+bls_pairing.h's Jacobian ones; the lines are the same lines up to Fp2 factors (2YZ for a
+tangent, Z1 Z2^2 for a chord), which the final exponentiation kills, so the team loop's
+pairing value equals miller_loop1's (tests/test_hostsim_math.py compares final_exp):
 
-  init  (once per pair)  miller_jq_make: zz = Z2^2, xz = X2 Z2, zzz = Z2^3, zzz*xn, zzz*yp
-  dbl   3 rounds         miller_dbl: T <- 2T, line (l0, l1, l3)
-  add   5 rounds         miller_add_jq: T <- T + Q, line
+  init  (once per pair)  Q -> (QX QZ, QY, QZ^3) into bank 0 and the constants below  3 rounds
+  dbl   2 rounds   R1: XY, B = Y^2, YZ, U = 3b'Z^2, A = X^2
+                   R2: X3 = 2XY (B - 3U), Y3 = B (B + 6U) - 3U^2, Z3 = 8B YZ,
+                       l0 = (B - U) Z_P^3, l1 = 3A (-X_P Z_P), l3 = 2YZ Y_P  (tangent x 2YZ)
+  add   3 rounds   tools/gen_tcurve.py's projective addition with Q; u = Y2Z1 - Y1Z2,
+                   v = X2Z1 - X1Z2 (Q = (X2, Y2, Z2)); R3 adds the chord
+                       l0 = u X2 Z_P^3 - v Y2 Z_P^3, l1 = u Z2 (-X_P Z_P), l3 = v Z2 Y_P
 
 The generator tracks an upper bound (in units of p) for every slot and checks each
 instruction against the reduction's input range, so no lin() or sum can leave the
@@ -29,12 +36,14 @@ MAX_LIN = 6        # slots per lin()
 # ---- fixed slots --------------------------------------------------------------------------
 ONE, XN, YP = 0, 1, 2                       # Montgomery 1, -X_P Z_P, Y_P (P Jacobian)
 QX, QY, QZ = (3, 4), (5, 6), (7, 8)         # Q (Jacobian)
-ZZ, XZ, ZZZ, ZZZ_XN, ZZZ_YP = (9, 10), (11, 12), (13, 14), (15, 16), (17, 18)
+# Q in homogeneous projective form (QPX, QY, QPZ) and the add lines' constants:
+# X2Z = QPX Z_P^3, CX = QPZ (-X_P Z_P), CY = QPZ Y_P, Y2Z = QY Z_P^3
+QPX, QPZ, X2Z, CX, CY = (9, 10), (11, 12), (13, 14), (15, 16), (17, 18)
 BANK = [((19, 20), (21, 22), (23, 24)), ((25, 26), (27, 28), (29, 30))]  # T = (X, Y, Z)
 L0, L1, L3 = (31, 32), (33, 34), (35, 36)   # the step's line
 DUMMY = 37
 ZP3 = 38                                    # Z_P^3 (lines scaled by it, bls_pairing.h miller_p)
-Y2S = (39, 40)                              # Y2 Z_P^3
+Y2Z = (39, 40)
 TEMP0 = 41
 
 INPUT_BOUND = {ONE: 1, XN: 2, YP: 2, ZP3: 2}
@@ -153,22 +162,26 @@ def lin2(*terms):
 
 def prog_init():
     g = Prog("init", INPUT_BOUND)
-    Q = {"x": pair(QX), "y": pair(QY), "z": pair(QZ)}
-    zz = g.sqr2(Q["z"], out=ZZ)
-    xz = g.mul2(Q["x"], Q["z"])
-    g.mulfp(Q["y"], S(ZP3), out=Y2S)
+    QXp, QYp, QZp = pair(QX), pair(QY), pair(QZ)
+    X0, Y0, Z0 = BANK[0]
+    g.mul2(QXp, QZp, out=QPX)
+    g.mul2(QXp, QZp, out=X0)
+    g.ident2(QYp, Y0)
+    zz = g.sqr2(QZp)
+    g.mulfp(QYp, S(ZP3), out=Y2Z)
     g.new_round()
-    zzz = g.mul2(zz, Q["z"], out=ZZZ)
-    g.mulfp(xz, S(ZP3), out=XZ)
+    g.mul2(QZp, zz, out=QPZ)
+    g.mul2(QZp, zz, out=Z0)
+    g.mulfp(pair(QPX), S(ZP3), out=X2Z)
     g.new_round()
-    g.mulfp(zzz, S(XN), out=ZZZ_XN)
-    g.mulfp(zzz, S(YP), out=ZZZ_YP)
+    g.mulfp(pair(QPZ), S(XN), out=CX)
+    g.mulfp(pair(QPZ), S(YP), out=CY)
     return g
 
 
 def base_bounds(src_bank, init):
     b = dict(INPUT_BOUND)
-    for s in ZZ + XZ + ZZZ + ZZZ_XN + ZZZ_YP + Y2S:
+    for s in QPX + QPZ + X2Z + CX + CY + Y2Z:
         b[s] = init.bound[s]
     for t in BANK[src_bank]:
         for s in t:
@@ -176,84 +189,65 @@ def base_bounds(src_bank, init):
     return b
 
 
+def mul_b3(a):
+    """3 b' a = 12 (1 + u) a (b' = 4 (1 + u), the twist's constant)"""
+    return (scale(add(a[0], scale(a[1], -1)), 12), scale(add(a[0], a[1]), 12))
+
+
+def neg_prod(c, d):
+    """-(c d) as extra product terms of mul2 (re, im)"""
+    return ([(scale(c[0], -1), d[0]), (c[1], d[1])], [(scale(c[0], -1), d[1]), (scale(c[1], -1), d[0])])
+
+
 def prog_dbl(src, init, bank_bound):
-    """miller_dbl (bls_pairing.h:11-28) over bank src -> bank 1 - src"""
+    """T <- 2T over bank src -> bank 1 - src with the tangent line (projective)"""
     g = Prog("dbl%d" % src, {**base_bounds(src, init), **bank_bound})
     X, Y, Z = (pair(t) for t in BANK[src])
     X3o, Y3o, Z3o = BANK[1 - src]
-    # R1: A = X^2, B = Y^2, ZZ = Z^2, Z3 = (Y + Z)^2 - B - ZZ = 2 Y Z
-    A = g.sqr2(X)
+    XY = g.mul2(X, Y)
     B = g.sqr2(Y)
-    ZZl = g.sqr2(Z)
-    Z3 = g.mul2(lin2((2, Y)), Z, out=Z3o)
+    YZ = g.mul2(Y, Z)
+    U = g.mul2(Z, mul_b3(Z))
+    A = g.sqr2(X)
     g.new_round()
-    # R2: C = B^2, G = (X + B)^2, F = E^2 (E = 3A), l0 = E X - 2B, EZZ = E ZZ, Z3ZZ = Z3 ZZ
-    C = g.sqr2(B)
-    G = g.sqr2(lin2((1, X), (1, B)))
-    F = g.sqr2(lin2((3, A)))
-    E = lin2((3, A))
-    EX = g.mul2(E, X)
-    EZZ = g.mul2(E, ZZl)
-    Z3ZZ = g.mul2(Z3, ZZl)
-    g.new_round()
-    # R3: D = 2(G - A - C); X3 = F - 2D; Y3 = E (D - X3) - 8C; l1 = EZZ xn; l3 = Z3ZZ yp
-    D = lin2((2, G), (-2, A), (-2, C))
-    X3 = lin2((1, F), (-4, G), (4, A), (4, C))
-    g.ident2(X3, X3o)
-    DmX3 = lin2((6, G), (-6, A), (-6, C), (-1, F))
-    negC8 = lin2((-8, C))
-    g.mul2(E, DmX3, out=Y3o, extra=([(negC8[0], S(ONE))], [(negC8[1], S(ONE))]))
-    g.mulfp(EZZ, S(XN), out=L1)
-    g.mulfp(Z3ZZ, S(YP), out=L3)
-    g.mulfp(lin2((1, EX), (-2, B)), S(ZP3), out=L0)   # (E X - 2B) Z_P^3
-    del D
+    g.mul2(lin2((2, XY)), lin2((1, B), (-3, U)), out=X3o)
+    g.mul2(B, lin2((1, B), (6, U)), out=Y3o, extra=neg_prod(lin2((3, U)), U))
+    g.mul2(lin2((8, B)), YZ, out=Z3o)
+    g.mulfp(lin2((1, B), (-1, U)), S(ZP3), out=L0)
+    g.mulfp(lin2((3, A)), S(XN), out=L1)
+    g.mulfp(lin2((2, YZ)), S(YP), out=L3)
     return g
 
 
 def prog_add(src, init, bank_bound):
-    """miller_add_jq (bls_pairing.h:99-120) over bank src -> bank 1 - src"""
+    """T <- T + Q over bank src -> bank 1 - src with the chord line (projective)"""
     g = Prog("add%d" % src, {**base_bounds(src, init), **bank_bound})
-    X, Y, Z = (pair(t) for t in BANK[src])
+    X1, Y1, Z1 = (pair(t) for t in BANK[src])
+    X2, Y2, Z2 = pair(QPX), pair(QY), pair(QPZ)
     X3o, Y3o, Z3o = BANK[1 - src]
-    q = {"x": pair(QX), "y": pair(QY), "z": pair(QZ)}
-    zz, xz, zzz, zzz_xn, zzz_yp = pair(ZZ), pair(XZ), pair(ZZZ), pair(ZZZ_XN), pair(ZZZ_YP)
-    # R1: ZZ = Z^2, U1 = X zz, S1 = Y zz Z2 (= Y zzz), Z3' = (Z + Z2)^2 - ZZ - zz = 2 Z Z2, Y2Z = Y2 Z
-    ZZl = g.sqr2(Z)
-    U1 = g.mul2(X, zz)
-    S1 = g.mul2(Y, zzz)
-    Z3p = g.mul2(lin2((2, Z)), q["z"])
-    Y2Z = g.mul2(q["y"], Z)
+    A1 = g.mul2(Y2, Z1)
+    A2 = g.mul2(Y1, Z2)
+    B1 = g.mul2(X2, Z1)
+    B2 = g.mul2(X1, Z2)
+    ZZ = g.mul2(Z1, Z2)
     g.new_round()
-    # R2: U2 = X2 ZZ, S2 = Y2 Z ZZ
-    U2 = g.mul2(q["x"], ZZl)
-    S2 = g.mul2(Y2Z, ZZl)
+    u = lin2((1, A1), (-1, A2))
+    v = lin2((1, B1), (-1, B2))
+    uu = g.sqr2(u)
+    vv = g.sqr2(v)
+    vZZ = g.mul2(v, ZZ)
+    vB2 = g.mul2(v, B2)
+    uB2 = g.mul2(u, B2)
+    uZZ = g.mul2(u, ZZ)
+    uv = g.mul2(u, v)
+    vA2 = g.mul2(v, A2)
     g.new_round()
-    # R3: H = U2 - U1, HH = H^2, r = 2(S2 - S1), rr = r^2, Z3 = Z3' H
-    H = lin2((1, U2), (-1, U1))
-    r = lin2((2, S2), (-2, S1))
-    HH = g.sqr2(H)
-    rr = g.sqr2(r)
-    Z3 = g.mul2(Z3p, H, out=Z3o)
-    g.new_round()
-    # R4: J = H I = 4 H HH, V = U1 I = 4 U1 HH, l0 = r xz - Y2 Z3 (xz, Y2 scaled by Z_P^3),
-    # l1 = r zzz_xn, l3 = Z3 zzz_yp
-    J = g.mul2(lin2((4, H)), HH)
-    V = g.mul2(lin2((4, U1)), HH)
-    y2s = pair(Y2S)
-    nY2 = lin2((-1, y2s))
-    g.mul2(r, xz, out=L0, extra=([(nY2[0], Z3[0]), (y2s[1], Z3[1])],
-                                 [(nY2[0], Z3[1]), (nY2[1], Z3[0])]))
-    g.mul2(r, zzz_xn, out=L1)
-    g.mul2(Z3, zzz_yp, out=L3)
-    g.new_round()
-    # R5: X3 = r^2 - J - 2V, Y3 = r (V - X3) - 2 S1 J
-    X3 = lin2((1, rr), (-1, J), (-2, V))
-    g.ident2(X3, X3o)
-    VmX3 = lin2((3, V), (-1, rr), (1, J))
-    nS1 = lin2((-2, S1))
-    # -2 S1 J = (-2 S1_0 J_0 + 2 S1_1 J_1) + (-2 S1_0 J_1 - 2 S1_1 J_0) u
-    g.mul2(r, VmX3, out=Y3o, extra=([(nS1[0], J[0]), (scale(S1[1], 2), J[1])],
-                                    [(nS1[0], J[1]), (nS1[1], J[0])]))
+    g.mul2(uu, vZZ, out=X3o, extra=neg_prod(vv, lin2((1, vv), (2, vB2))))
+    g.mul2(vv, lin2((3, uB2), (1, uv), (-1, vA2)), out=Y3o, extra=neg_prod(uu, uZZ))
+    g.mul2(vv, vZZ, out=Z3o)
+    g.mul2(u, pair(X2Z), out=L0, extra=neg_prod(v, pair(Y2Z)))
+    g.mul2(u, pair(CX), out=L1)
+    g.mul2(v, pair(CY), out=L3)
     return g
 
 
