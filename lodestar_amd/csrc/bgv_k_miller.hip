@@ -243,7 +243,14 @@ __global__ void __launch_bounds__(128) k_miller_wide(const bgv_dslot* __restrict
   auto post = [&](int r, int k) {
     if (lane < 6) LR[r][k][lane] = Sm[(lane < 2 ? TMP_S_L0 : (lane < 4 ? TMP_S_L1 - 2 : TMP_S_L3 - 4)) + lane];
   };
-  tm_wide_ops_t<true> o{WA, WB, WP, lane % BGV_TEAM_COMPS, lane / BGV_TEAM_COMPS};
+  // the Fp12 accumulator's squarings from the lane's operand recipes (bls_team.h tm_sqr_rec4)
+  tm_wide4_lean_ops o;
+  o.A = WA;
+  o.B = WB;
+  o.P = WP;
+  o.c = lane % BGV_TEAM_COMPS;
+  o.q = lane / BGV_TEAM_COMPS;
+  tm_sqr_rec4(o.c, o.q < 4 ? o.q : 3, &o.x1, &o.y1, &o.x2, &o.y2);
   auto ln = [&](int r, int k, fp2_t* l0, fp2_t* l1, fp2_t* l3) {
     const fp_t* L = LR[r][k];
     *l0 = fp2_t{L[0], L[1]};

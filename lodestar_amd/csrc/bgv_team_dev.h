@@ -169,3 +169,16 @@ struct tm_wide8_lean_ops : tm_wide_ops_t<false, 8> {
     return gather();
   }
 };
+
+// Four-part one-wave ops (k_miller_wide) with the lean squaring (bls_team.h tm_sqr_rec4):
+// the lane's four operand recipes fixed once.  Same parts, bit for bit.
+struct tm_wide4_lean_ops : tm_wide_ops_t<true, 4> {
+  tm_lin_t x1, y1, x2, y2;
+  __device__ fp_t sqr(const fp_t& x) {
+    if (q == 0) A[c] = x;
+    sync();
+    if (q < 4) P[q * BGV_TEAM_COMPS + c] = tm_sqr_part4_lean(A, x1, y1, x2, y2);
+    sync();
+    return gather();
+  }
+};

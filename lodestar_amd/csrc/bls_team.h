@@ -344,6 +344,22 @@ BGV_HD fp_t tm_sqr_part8_lean(const fp_t* A, const tm_lin_t& X, const tm_lin_t& 
   return wide_redc(t);
 }
 
+// The four-part squaring (tm_sqr_part) from the same recipes: part q < 3 is pair q's two
+// products (eight-part recipes 2q, 2q + 1), part 3 the diagonal (recipes 6, 7).
+BGV_HD void tm_sqr_rec4(int c, int q, tm_lin_t* X1, tm_lin_t* Y1, tm_lin_t* X2, tm_lin_t* Y2) {
+  tm_sqr_rec8(c, 2 * q, X1, Y1);
+  tm_sqr_rec8(c, 2 * q + 1, X2, Y2);
+}
+
+BGV_HD fp_t tm_sqr_part4_lean(const fp_t* A, const tm_lin_t& X1, const tm_lin_t& Y1, const tm_lin_t& X2,
+                              const tm_lin_t& Y2) {
+  uint64_t t[2 * NL];
+  BGV_UNROLL for (int z = 0; z < 2 * NL; ++z) t[z] = 0;
+  wide_mac(t, tm_lin(A, X1), tm_lin(A, Y1));
+  wide_mac(t, tm_lin(A, X2), tm_lin(A, Y2));
+  return wide_redc(t);
+}
+
 BGV_HD fp_t tm_mul_line_part8(int c, int q, const fp_t* A, const fp2_t& l0, const fp2_t& l1, const fp2_t& l3) {
   const int k = c >> 1, e = c & 1;
   uint64_t t[2 * NL];

@@ -303,6 +303,23 @@ int hs_team_sqr8_lean_diff(const uint8_t* a) {
     }
   return bad;
 }
+// the lean four-part squaring (k_miller_wide): parts differing from tm_sqr_part, limb for limb
+int hs_team_sqr4_lean_diff(const uint8_t* a) {
+  const tm_emu_t x = tm_emu_from_fp12(in_fp12(a));
+  int bad = 0;
+  for (int c = 0; c < BGV_TEAM_COMPS; ++c)
+    for (int q = 0; q < 4; ++q) {
+      tm_lin_t X1, Y1, X2, Y2;
+      tm_sqr_rec4(c, q, &X1, &Y1, &X2, &Y2);
+      const fp_t u = tm_sqr_part(c, q, x.c), v = tm_sqr_part4_lean(x.c, X1, Y1, X2, Y2);
+      for (int l = 0; l < NL; ++l)
+        if (u.v[l] != v.v[l]) {
+          ++bad;
+          break;
+        }
+    }
+  return bad;
+}
 int hs_team_final_is_one_wide8_lean(const uint8_t* f) {
   tm_emu_wide8_lean_ops o;
   return tm_final_exp_is_one(o, tm_emu_from_fp12(in_fp12(f)));

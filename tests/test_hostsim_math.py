@@ -422,6 +422,7 @@ def test_team_fp12_ops(L):
         L.hs_team_sqr_wide8_lean(got, a)  # operand recipes per lane (k_final_fold)
         assert got.raw == want.raw
         assert L.hs_team_sqr8_lean_diff(a) == 0  # the same 96 parts, limb for limb
+        assert L.hs_team_sqr4_lean_diff(a) == 0  # the four-part form (k_miller_wide)
         for tf, ref in ((L.hs_team_frob, L.hs_fp12_frob), (L.hs_team_frob2, L.hs_fp12_frob2)):
             tf(got, a)
             ref(want, a)
