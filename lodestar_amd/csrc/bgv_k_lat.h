@@ -13,9 +13,10 @@ static __device__ __forceinline__ g2_aff* split_sig(fp12_t* f, uint32_t s) {
 }
 static_assert(sizeof(g2_jac) + sizeof(g2_aff) <= sizeof(fp12_t), "split intermediates fit in f[s]");
 
-// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), isogeny included.  PW: the
-// square roots' exponentiations on this lane (bgv_pow_lane) or on the whole wave (bgv_pow_wave,
-// one set per wave, every lane computing the same values; lane 0 writes).
+// one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), the point on E2' (Jacobian):
+// the 3-isogeny runs in the next launch's point programs (tools/gen_tcurve.py iso14 / iso25).
+// PW: the square roots' exponentiations on this lane (bgv_pow_lane) or on the whole wave
+// (bgv_pow_wave, one set per wave, every lane computing the same values; lane 0 writes).
 template <class PW>
 __device__ __noinline__ void task_map_t(uint32_t s, int which, const bgv_dslot* __restrict__ slots, g2_jac* out,
                                         bool writer) {
@@ -25,7 +26,7 @@ __device__ __noinline__ void task_map_t(uint32_t s, int which, const bgv_dslot* 
   for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, 32);
-  const g2_jac q = iso_map_g2_jac(sswu_g2_jac_t<PW>(which ? u1 : u0, fp_sqrt_minus5()));
+  const g2_jac q = sswu_g2_jac_t<PW>(which ? u1 : u0, fp_sqrt_minus5());
   if (writer) *out = q;
 }
 

@@ -203,6 +203,7 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
   } else if (c == 12) {
     S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
   }
+  for (int i = c; i < TC_ISO_NCONST; i += BGV_TEAM) S[TCP_S_ISO + i] = tc_iso_const(i);
   tc_dev_engine e{prog, S, c, false};
   if (blockIdx.y == 0) {
     if (c < 6) {
@@ -217,7 +218,7 @@ __global__ void __launch_bounds__(64) k_prep_team(const bgv_dslot* __restrict__ 
       if (!flags[team]) {
         if (c < 6) reinterpret_cast<fp_t*>(h + uu)[c] = S[TCP_BANK(3) + c];
       } else if (c == 0) {
-        h[uu] = g2_clear_cofactor(jac_add(h[uu], *split_q1(f, uu)));
+        h[uu] = g2_clear_cofactor(jac_add(iso_map_g2_jac(h[uu]), iso_map_g2_jac(*split_q1(f, uu))));
       }
     }
   } else {
@@ -323,6 +324,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
       S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
     }
   }
+  for (int i = lane; i < TC_ISO_NCONST; i += 64) S[TCP_S_ISO + i] = tc_iso_const(i);
   tc_wide_engine e{{prog, S, RP, c, q, false}};
   if (blockIdx.y == 0) {
     if (q == 0 && c < 6) {
@@ -337,7 +339,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
       if (!flag) {
         if (q == 0 && c < 6) reinterpret_cast<fp_t*>(h + uu)[c] = S[TCP_BANK(3) + c];
       } else if (lane == 0) {
-        h[uu] = g2_clear_cofactor(jac_add(h[uu], *split_q1(f, uu)));
+        h[uu] = g2_clear_cofactor(jac_add(iso_map_g2_jac(h[uu]), iso_map_g2_jac(*split_q1(f, uu))));
       }
     }
   } else if (blockIdx.y == 1) {
@@ -414,6 +416,7 @@ __global__ void __launch_bounds__(256) k_prep_wide4(const bgv_dslot* __restrict_
   } else if (t == 12) {
     S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
   }
+  for (int i = t; i < TC_ISO_NCONST; i += 256) S[TCP_S_ISO + i] = tc_iso_const(i);
   tc_wave4_engine e{prog, S, wr_init(), t / 64, false};
   if (blockIdx.y == 0) {
     if (t < 6) {
@@ -428,7 +431,7 @@ __global__ void __launch_bounds__(256) k_prep_wide4(const bgv_dslot* __restrict_
       if (!flag) {
         if (t < 6) reinterpret_cast<fp_t*>(h + uu)[t] = S[TCP_BANK(3) + t];
       } else if (t == 0) {
-        h[uu] = g2_clear_cofactor(jac_add(h[uu], *split_q1(f, uu)));
+        h[uu] = g2_clear_cofactor(jac_add(iso_map_g2_jac(h[uu]), iso_map_g2_jac(*split_q1(f, uu))));
       }
     }
   } else if (blockIdx.y == 1) {

@@ -24,6 +24,16 @@
 #define TC_CHK_A TCP_S_VV
 #define TC_CHK_B TCP_S_ZZ
 
+// The isogeny programs' constant slots: x_num[4], x_den[2], y_num[4], y_den[3] (Fp2, bls_hash.h
+// iso_map_g2_jac) as TC_ISO_NCONST Fp values from TCP_S_ISO on; every engine's slots hold them.
+#define TC_ISO_NCONST 26
+BGV_HD fp_t tc_iso_const(int i) {
+  const fp2_t xn[4] = BGV_ISO_XNUM, xd[2] = BGV_ISO_XDEN, yn[4] = BGV_ISO_YNUM, yd[3] = BGV_ISO_YDEN;
+  const int k = i >> 1;
+  const fp2_t& v = k < 4 ? xn[k] : (k < 6 ? xd[k - 4] : (k < 10 ? yn[k - 6] : yd[k - 10]));
+  return (i & 1) ? v.c1 : v.c0;
+}
+
 // the projective point in bank b -> Jacobian in bank 1 (returns 1)
 template <class E>
 BGV_HD int tc_to_jac(E& e, int b) {
@@ -49,12 +59,13 @@ BGV_HD int tc_mul_x_abs(E& e) {
   return acc;
 }
 
-// RFC 9380 G.4 (bls_curve.h g2_clear_cofactor) of q0 + q1: q0 in bank 1, q1 in bank 2 on
-// entry (Jacobian), the result in bank 3 (Jacobian).  Storage banks: 6 = P, 7 = t1, 8 = t2,
-// 9 = t3.
+// RFC 9380 G.4 (bls_curve.h g2_clear_cofactor) of iso(q0) + iso(q1): the SSWU points q0 in
+// bank 1, q1 in bank 2 on entry (on E2', Jacobian), the result in bank 3 (Jacobian).  Storage
+// banks: 6 = P, 7 = t1, 8 = t2, 9 = t3.
 template <class E>
 BGV_HD void tc_clear_cofactor(E& e) {
-  e.run(TCP_J2P12_45);  // q0, q1 -> projective
+  e.run(TCP_ISO14);  // the 3-isogeny of q0, q1 into projective banks 4, 5
+  e.run(TCP_ISO25);
   e.copy(1, 4);
   e.copy(2, 5);
   e.run(TCP_PADD123);  // P = q0 + q1
@@ -201,6 +212,7 @@ struct tc_host_engine {
 
 inline void tc_host_init(fp_t* S) {
   for (int i = 0; i < TCP_NSLOT; ++i) S[i] = fp_zero();
+  for (int i = 0; i < TC_ISO_NCONST; ++i) S[TCP_S_ISO + i] = tc_iso_const(i);
   const fp2_t cx = BGV_PSI_CX, cy = BGV_PSI_CY;
   S[TCP_S_ONE] = fp_one();
   S[TCP_S_PSI_CX] = cx.c0;
@@ -220,8 +232,8 @@ inline g2_jac tc_get(const fp_t* S, int b) {
   return g2_jac{fp2_t{v[0], v[1]}, fp2_t{v[2], v[3]}, fp2_t{v[4], v[5]}};
 }
 
-// g2_clear_cofactor(q0 + q1) and [k]P through the team schedules (*bad: the cofactor
-// clearing met an exceptional addition)
+// g2_clear_cofactor(iso(q0) + iso(q1)) of two SSWU points and [k]P through the team schedules
+// (*bad: the cofactor clearing met an exceptional addition)
 inline g2_jac tc_clear_cofactor_host(const g2_jac& q0, const g2_jac& q1, bool* bad) {
   static const uint8_t tab[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
   static fp_t S[TCP_NSLOT];

@@ -359,7 +359,7 @@ int hs_tcurve_check(const uint8_t* msg32, uint64_t k, int* bad_out) {
       !jac_eq(q1, iso_map_g2_jac(sswu_g2_jac(u1, fp_sqrt_minus5()))))
     return 0;
   bool bad;
-  const g2_jac h_team = tc_clear_cofactor_host(q0, q1, &bad);
+  const g2_jac h_team = tc_clear_cofactor_host(sswu_g2_jac(u0, fp_sqrt_minus5()), sswu_g2_jac(u1, fp_sqrt_minus5()), &bad);
   const g2_jac h_lane = g2_clear_cofactor(jac_add(q0, q1));
   *bad_out = bad;
   if (!jac_eq(h_team, h_lane)) return 0;

@@ -47,12 +47,21 @@ def bank(k):
     return ((b, b + 1), (b + 2, b + 3), (b + 4, b + 5))
 
 
-TEMP0 = BANK0 + 6 * NBANK
+# the 3-isogeny's constants (RFC 9380 E.3, bls_hash.h iso_map_g2_jac), Fp2 pairs after the banks:
+# x_num k1_0..3, x_den k2_0..1 (x^2 monic), y_num k3_0..3, y_den k4_0..2 (x^3 monic)
+ISO0 = BANK0 + 6 * NBANK
+ISO_XN = [(ISO0 + 2 * i, ISO0 + 2 * i + 1) for i in range(4)]
+ISO_XD = [(ISO0 + 8 + 2 * i, ISO0 + 9 + 2 * i) for i in range(2)]
+ISO_YN = [(ISO0 + 12 + 2 * i, ISO0 + 13 + 2 * i) for i in range(4)]
+ISO_YD = [(ISO0 + 20 + 2 * i, ISO0 + 21 + 2 * i) for i in range(3)]
+TEMP0 = ISO0 + 26
 gm.TEMP0 = TEMP0  # Prog allocates temporaries from here
 gm.ONE = ONE
 gm.DUMMY = DUMMY
 
 BOUND_IN = {ONE: 1, PSI_CX[0]: 1, PSI_CX[1]: 1, PSI_CY[0]: 1, PSI_CY[1]: 1, PSI2_CX: 1, PSI2_CY: 1}
+for _t in ISO_XN + ISO_XD + ISO_YN + ISO_YD:
+    BOUND_IN[_t[0]] = BOUND_IN[_t[1]] = 1
 PT_BOUND = 2.0  # every bank value is weakly reduced (< 2p): checked on every program's outputs
 
 
@@ -119,6 +128,57 @@ def prog_padd(a, b, dst):
     g.mul2(vv, lin2((3, uB2), (1, uv), (-1, vA2)), out=Y3o, extra=neg_prod(uu, uZZ))
     g.mul2(vv, vZZ, out=Z3o)
     CHK_SLOTS[g.name] = (list(vv[0])[0], list(ZZ[0])[0])
+    return g
+
+
+def pos_prod(c, d):
+    """+(c d) as extra product terms of mul2 (re, im)"""
+    return ([(c[0], d[0]), (scale(c[1], -1), d[1])], [(c[0], d[1]), (c[1], d[0])])
+
+
+def cat(*ts):
+    return (sum((list(t[0]) for t in ts), []), sum((list(t[1]) for t in ts), []))
+
+
+def prog_iso(src, dst):
+    """The 3-isogeny E2' -> E2 of an SSWU point (Jacobian, bank src) into projective bank dst:
+    with z2 = Z^2 and the maps homogenized (XNh = x_num z2^3, XDh = x_den z2^2, YNh = y_num z2^3,
+    YDh = y_den z2^3), X' = XNh Z^3 YDh, Y' = Y YNh XDh z2, Z' = XDh z2 Z^3 YDh   6 rounds"""
+    g = Prog("iso%d%d" % (src, dst), bounds_with(src))
+    X, Y, Z = (pair(t) for t in bank(src))
+    X3o, Y3o, Z3o = bank(dst)
+    k1 = [pair(t) for t in ISO_XN]
+    k2 = [pair(t) for t in ISO_XD]
+    k3 = [pair(t) for t in ISO_YN]
+    k4 = [pair(t) for t in ISO_YD]
+    one = (S(ONE), S(ONE))
+    z2 = g.sqr2(Z)
+    X2 = g.sqr2(X)
+    g.new_round()
+    X3 = g.mul2(X2, X)
+    X2z2 = g.mul2(X2, z2)
+    Xz2 = g.mul2(X, z2)
+    z4 = g.sqr2(z2)
+    Z3 = g.mul2(Z, z2)
+    Yz2 = g.mul2(Y, z2)
+    g.new_round()
+    Xz4 = g.mul2(Xz2, z2)
+    z6 = g.mul2(z4, z2)
+    XD = g.mul2(k2[1], Xz2, extra=cat(pos_prod(k2[0], z4), ([(X2[0], S(ONE))], [(X2[1], S(ONE))])))
+    g.new_round()
+    XN = g.mul2(k1[3], X3, extra=cat(pos_prod(k1[2], X2z2), pos_prod(k1[1], Xz4), pos_prod(k1[0], z6)))
+    YN = g.mul2(k3[3], X3, extra=cat(pos_prod(k3[2], X2z2), pos_prod(k3[1], Xz4), pos_prod(k3[0], z6)))
+    YD = g.mul2(k4[2], X2z2, extra=cat(pos_prod(k4[1], Xz4), pos_prod(k4[0], z6),
+                                        ([(X3[0], S(ONE))], [(X3[1], S(ONE))])))
+    W1 = g.mul2(Yz2, XD)
+    XDz2 = g.mul2(XD, z2)
+    g.new_round()
+    Z3YD = g.mul2(Z3, YD)
+    g.mul2(W1, YN, out=Y3o)
+    g.new_round()
+    g.mul2(XN, Z3YD, out=X3o)
+    g.mul2(XDz2, Z3YD, out=Z3o)
+    del one
     return g
 
 
@@ -211,7 +271,8 @@ def emit(progs):
          "#define TCP_NSLOT %d" % nslots,
          "#define TCP_S_ONE %d" % ONE, "#define TCP_S_PSI_CX %d" % PSI_CX[0], "#define TCP_S_PSI_CY %d" % PSI_CY[0],
          "#define TCP_S_PSI2_CX %d" % PSI2_CX, "#define TCP_S_PSI2_CY %d" % PSI2_CY,
-         "#define TCP_S_DUMMY %d" % DUMMY, "#define TCP_BANK(k) (%d + 6 * (k))" % BANK0]
+         "#define TCP_S_DUMMY %d" % DUMMY, "#define TCP_BANK(k) (%d + 6 * (k))" % BANK0,
+         "#define TCP_S_ISO %d  // x_num[4], x_den[2], y_num[4], y_den[3] (Fp2 pairs)" % ISO0]
     for name, off in offsets.items():
         L.append("#define TCP_%s %d" % (name.upper(), off))
     chk = set(CHK_SLOTS.values())
@@ -225,7 +286,8 @@ def emit(progs):
 
 def main():
     progs = [prog_pdbl(4, 5), prog_pdbl(5, 4), prog_padd(4, 0, 5), prog_padd(5, 0, 4), prog_padd(1, 2, 3),
-             prog_psi(1, 2), prog_psi2(1, 2), prog_j2p([(1, 4), (2, 5)], "j2p12_45"), prog_p2j(3, 1)]
+             prog_psi(1, 2), prog_psi2(1, 2), prog_j2p([(1, 4), (2, 5)], "j2p12_45"), prog_p2j(3, 1),
+             prog_iso(1, 4), prog_iso(2, 5)]
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lodestar_amd", "csrc",
                        "bgv_tcurve_prog.h")
     open(out, "w").write(emit(progs))
