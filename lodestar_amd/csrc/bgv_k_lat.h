@@ -14,7 +14,7 @@ static __device__ __forceinline__ g2_aff* split_sig(fp12_t* f, uint32_t s) {
 static_assert(sizeof(g2_jac) + sizeof(g2_aff) <= sizeof(fp12_t), "split intermediates fit in f[s]");
 
 // one of the two SSWU maps of hash_to_G2 (bls_hash.h hash_to_g2), the point on E2' (Jacobian):
-// the 3-isogeny runs in the next launch's point programs (tools/gen_tcurve.py iso14 / iso25).
+// the 3-isogeny runs in the next launch's point programs (tools/gen_tcurve.py iso12_45).
 // PW: the square roots' exponentiations on this lane (bgv_pow_lane) or on the whole wave
 // (bgv_pow_wave, one set per wave, every lane computing the same values; lane 0 writes).
 template <class PW>

@@ -64,8 +64,7 @@ BGV_HD int tc_mul_x_abs(E& e) {
 // banks: 6 = P, 7 = t1, 8 = t2, 9 = t3.
 template <class E>
 BGV_HD void tc_clear_cofactor(E& e) {
-  e.run(TCP_ISO14);  // the 3-isogeny of q0, q1 into projective banks 4, 5
-  e.run(TCP_ISO25);
+  e.run(TCP_ISO12_45);  // the 3-isogeny of q0, q1 into projective banks 4, 5
   e.copy(1, 4);
   e.copy(2, 5);
   e.run(TCP_PADD123);  // P = q0 + q1

@@ -17,6 +17,8 @@ fewer rounds (a round squares the degree at most):
                     (Jacobian add-2007-bl: 5)
   psi12 / psi2_12   g2_psi / g2_psi2: the same maps in either coordinates               1 round
   j2p12_45          Jacobian banks 1, 2 -> projective banks 4, 5: (XZ, Y, Z^3)         2 rounds
+  iso12_45          the 3-isogeny of the SSWU points in banks 1, 2 (E2', Jacobian) into
+                    projective banks 4, 5, both points side by side                     6 rounds
   p2j31             projective bank 3 -> Jacobian bank 1: (XZ, YZ^2, Z)                2 rounds
 
 The schedules convert at their entry and exit, so every bank handed in or out is Jacobian,
@@ -140,45 +142,57 @@ def cat(*ts):
     return (sum((list(t[0]) for t in ts), []), sum((list(t[1]) for t in ts), []))
 
 
-def prog_iso(src, dst):
-    """The 3-isogeny E2' -> E2 of an SSWU point (Jacobian, bank src) into projective bank dst:
-    with z2 = Z^2 and the maps homogenized (XNh = x_num z2^3, XDh = x_den z2^2, YNh = y_num z2^3,
-    YDh = y_den z2^3), X' = XNh Z^3 YDh, Y' = Y YNh XDh z2, Z' = XDh z2 Z^3 YDh   6 rounds"""
-    g = Prog("iso%d%d" % (src, dst), bounds_with(src))
-    X, Y, Z = (pair(t) for t in bank(src))
-    X3o, Y3o, Z3o = bank(dst)
+def prog_iso(pairs, name):
+    """The 3-isogeny E2' -> E2 of SSWU points (Jacobian, banks src) into projective banks dst,
+    both maps' points side by side: with z2 = Z^2 and the maps homogenized (XNh = x_num z2^3,
+    XDh = x_den z2^2, YNh = y_num z2^3, YDh = y_den z2^3), X' = XNh Z^3 YDh,
+    Y' = Y YNh XDh z2, Z' = XDh z2 Z^3 YDh.  6 rounds, at most 16 instructions each."""
+    g = Prog(name, bounds_with(*[s for s, _ in pairs]))
     k1 = [pair(t) for t in ISO_XN]
     k2 = [pair(t) for t in ISO_XD]
     k3 = [pair(t) for t in ISO_YN]
     k4 = [pair(t) for t in ISO_YD]
-    one = (S(ONE), S(ONE))
-    z2 = g.sqr2(Z)
-    X2 = g.sqr2(X)
+    st = {}
+    for src, dst in pairs:
+        X, Y, Z = (pair(t) for t in bank(src))
+        st[src] = {"X": X, "Y": Y, "Z": Z, "z2": g.sqr2(Z), "X2": g.sqr2(X)}
     g.new_round()
-    X3 = g.mul2(X2, X)
-    X2z2 = g.mul2(X2, z2)
-    Xz2 = g.mul2(X, z2)
-    z4 = g.sqr2(z2)
-    Z3 = g.mul2(Z, z2)
-    Yz2 = g.mul2(Y, z2)
+    for src, _ in pairs:
+        v = st[src]
+        v["X3"] = g.mul2(v["X2"], v["X"])
+        v["X2z2"] = g.mul2(v["X2"], v["z2"])
+        v["Xz2"] = g.mul2(v["X"], v["z2"])
+        v["z4"] = g.sqr2(v["z2"])
     g.new_round()
-    Xz4 = g.mul2(Xz2, z2)
-    z6 = g.mul2(z4, z2)
-    XD = g.mul2(k2[1], Xz2, extra=cat(pos_prod(k2[0], z4), ([(X2[0], S(ONE))], [(X2[1], S(ONE))])))
+    for src, _ in pairs:
+        v = st[src]
+        v["Xz4"] = g.mul2(v["Xz2"], v["z2"])
+        v["z6"] = g.mul2(v["z4"], v["z2"])
+        v["XD"] = g.mul2(k2[1], v["Xz2"], extra=cat(pos_prod(k2[0], v["z4"]),
+                                                   ([(v["X2"][0], S(ONE))], [(v["X2"][1], S(ONE))])))
+        v["Z3"] = g.mul2(v["Z"], v["z2"])
     g.new_round()
-    XN = g.mul2(k1[3], X3, extra=cat(pos_prod(k1[2], X2z2), pos_prod(k1[1], Xz4), pos_prod(k1[0], z6)))
-    YN = g.mul2(k3[3], X3, extra=cat(pos_prod(k3[2], X2z2), pos_prod(k3[1], Xz4), pos_prod(k3[0], z6)))
-    YD = g.mul2(k4[2], X2z2, extra=cat(pos_prod(k4[1], Xz4), pos_prod(k4[0], z6),
-                                        ([(X3[0], S(ONE))], [(X3[1], S(ONE))])))
-    W1 = g.mul2(Yz2, XD)
-    XDz2 = g.mul2(XD, z2)
+    for src, _ in pairs:
+        v = st[src]
+        v["XN"] = g.mul2(k1[3], v["X3"], extra=cat(pos_prod(k1[2], v["X2z2"]), pos_prod(k1[1], v["Xz4"]),
+                                                  pos_prod(k1[0], v["z6"])))
+        v["YN"] = g.mul2(k3[3], v["X3"], extra=cat(pos_prod(k3[2], v["X2z2"]), pos_prod(k3[1], v["Xz4"]),
+                                                  pos_prod(k3[0], v["z6"])))
+        v["YD"] = g.mul2(k4[2], v["X2z2"], extra=cat(pos_prod(k4[1], v["Xz4"]), pos_prod(k4[0], v["z6"]),
+                                                    ([(v["X3"][0], S(ONE))], [(v["X3"][1], S(ONE))])))
+        v["XDz2"] = g.mul2(v["XD"], v["z2"])
     g.new_round()
-    Z3YD = g.mul2(Z3, YD)
-    g.mul2(W1, YN, out=Y3o)
+    for src, _ in pairs:
+        v = st[src]
+        v["Z3YD"] = g.mul2(v["Z3"], v["YD"])
+        v["W1"] = g.mul2(v["XDz2"], v["Y"])
     g.new_round()
-    g.mul2(XN, Z3YD, out=X3o)
-    g.mul2(XDz2, Z3YD, out=Z3o)
-    del one
+    for src, dst in pairs:
+        v = st[src]
+        X3o, Y3o, Z3o = bank(dst)
+        g.mul2(v["XN"], v["Z3YD"], out=X3o)
+        g.mul2(v["W1"], v["YN"], out=Y3o)
+        g.mul2(v["XDz2"], v["Z3YD"], out=Z3o)
     return g
 
 
@@ -287,7 +301,7 @@ def emit(progs):
 def main():
     progs = [prog_pdbl(4, 5), prog_pdbl(5, 4), prog_padd(4, 0, 5), prog_padd(5, 0, 4), prog_padd(1, 2, 3),
              prog_psi(1, 2), prog_psi2(1, 2), prog_j2p([(1, 4), (2, 5)], "j2p12_45"), prog_p2j(3, 1),
-             prog_iso(1, 4), prog_iso(2, 5)]
+             prog_iso([(1, 4), (2, 5)], "iso12_45")]
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lodestar_amd", "csrc",
                        "bgv_tcurve_prog.h")
     open(out, "w").write(emit(progs))
