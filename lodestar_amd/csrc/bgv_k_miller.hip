@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(128) k_miller_wide(const bgv_dslot* __restrict
     }
   }
   __syncthreads();
-  tr_wide_engine eng{prog, Sm, RP, lane % BGV_TEAM, lane / BGV_TEAM, false};
+  tr_wide_engine eng{prog, Sm, RP, tr_wide_lane_c(lane), tr_wide_lane_q(lane), false};
   // wave 0: the line of the last program run into ring entry (r, k)
   auto post = [&](int r, int k) {
     if (lane < 6) LR[r][k][lane] = Sm[(lane < 2 ? TMP_S_L0 : (lane < 4 ? TMP_S_L1 - 2 : TMP_S_L3 - 4)) + lane];

@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
     __syncthreads();
     if (!flag) return;  // uniform over the block
     const int lane = threadIdx.x;
-    tg1_wide_engine e{{prog, S, RP, lane % BGV_TEAM, lane / BGV_TEAM, false}};
+    tg1_wide_engine e{{prog, S, RP, tr_wide_lane_c(lane), tr_wide_lane_q(lane), false}};
     tg1_mul_glv(e, slots[s].scalar);
     if (lane < 3) reinterpret_cast<fp_t*>(rpk + s)[lane] = S[TG1_BANK(4) + lane];
     if (lane == 0) pk_status[s] = BGV_ST_OK;
@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
     }
   }
   for (int i = lane; i < TC_ISO_NCONST; i += 64) S[TCP_S_ISO + i] = tc_iso_const(i);
-  tc_wide_engine e{{prog, S, RP, c, q, false}};
+  tc_wide_engine e{{prog, S, RP, tr_wide_lane_c(lane), tr_wide_lane_q(lane), false}};
   if (blockIdx.y == 0) {
     if (q == 0 && c < 6) {
       S[TCP_BANK(1) + c] = reinterpret_cast<const fp_t*>(h + uu)[c];

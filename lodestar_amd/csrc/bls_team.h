@@ -381,11 +381,9 @@ BGV_HD fp_t tm_mul_line_part8(int c, int q, const fp_t* A, const fp2_t& l0, cons
   return wide_redc(t);
 }
 
-// sum of the four parts of a coefficient, back below 2p
-BGV_HD fp_t tm_sum4(const fp_t& a, const fp_t& b, const fp_t& c, const fp_t& d) {
-  fp_t r;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i] + c.v[i] + d.v[i];
-  // value < 8p, limbs < 2^30: one signed chain subtracting q p, q from the top limb (lz_out)
+// a limb-wise sum of four parts (value < 8p, limbs < 2^30) back below 2p: one signed chain
+// subtracting q p, q from the top limb (lz_out)
+BGV_HD fp_t tm_norm4(const fp_t& r) {
   const uint32_t P_[NL] = BGV_P_LIMBS;
   const uint32_t qt = r.v[NL - 1] / (uint32_t)(P_[NL - 1] + 1);
   int64_t cy = 0;
@@ -397,6 +395,13 @@ BGV_HD fp_t tm_sum4(const fp_t& a, const fp_t& b, const fp_t& c, const fp_t& d) 
   }
   o.v[NL - 1] = (uint32_t)((int64_t)r.v[NL - 1] - (int64_t)((uint64_t)qt * P_[NL - 1]) + cy);
   return o;
+}
+
+// sum of the four parts of a coefficient, back below 2p
+BGV_HD fp_t tm_sum4(const fp_t& a, const fp_t& b, const fp_t& c, const fp_t& d) {
+  fp_t r;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i] + c.v[i] + d.v[i];
+  return tm_norm4(r);
 }
 
 // sum of the eight parts of a coefficient (each < 1.07 p, limbs < 2^28.1), back below 2p by
