@@ -161,10 +161,10 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   if (live && c == 0) verdict[gi] = v;
 }
 
-// The latency path's closing (small calls): one 128-thread block of 8 teams per group.  Team t
-// multiplies the group's slots t, t + 8, ... (team 0 also the signature pair), the eight
-// partial products meet in LDS in a three-level tree (an eighth of k_final's serial product
-// chain).  The final exponentiation then runs on the
+// The latency path's closing (small calls): one block of BGV_FOLD_TEAMS (16) teams per group.
+// Team t multiplies the group's slots t, t + 16, ... (team 0 also the signature pair), the
+// partial products meet in LDS in a four-level tree (a sixteenth of k_final's serial product
+// chain; 8 teams measured 0.86 ms for the 64-set gossip call).  The final exponentiation then runs on the
 // whole block with each coefficient's products split over eight lanes (tm_wide_ops_t<false, 8>):
 // one double-width product per lane for a squaring (two for a product) instead of 7 on one.
 // LEAN: the squarings with the lane's operand recipes (bgv_team_dev.h tm_wide8_lean_ops; the
@@ -177,7 +177,10 @@ __device__ auto bgv_fold_ops_pick() {
   else
     return tm_wide_ops_t<false, 8>{};
 }
-#define BGV_FOLD_TEAMS 8  // 16-lane teams of k_final_fold's 128-thread block
+#ifndef BGV_FOLD_TEAMS
+#define BGV_FOLD_TEAMS 16  // 16-lane teams of k_final_fold's block (BGV_FOLD_THREADS threads)
+#endif
+#define BGV_FOLD_THREADS (BGV_FOLD_TEAMS * BGV_TEAM)
 template <bool LEAN>
 __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                                 const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
@@ -240,10 +243,10 @@ extern "C" {
   const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const fp12_t *__restrict__ f,                     \
       const fp12_t *__restrict__ gpair, int32_t *__restrict__ verdict, fp12_t *__restrict__ gprod,          \
       fp12_t *__restrict__ gu, const fp12_t *__restrict__ gu1, const fp12_t *__restrict__ fsig
-__global__ void __launch_bounds__(128) k_final_fold(BGV_FOLD_ARGS) {
+__global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold(BGV_FOLD_ARGS) {
   final_fold_body<true>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
 }
-__global__ void __launch_bounds__(128) k_final_fold_sel(BGV_FOLD_ARGS) {
+__global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold_sel(BGV_FOLD_ARGS) {
   final_fold_body<false>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
 }
 
@@ -320,7 +323,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     return !(e && atoi(e) == 0);
   }();
   if (b.nslots + b.ngroups <= bgv_latency_max())
-    hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(128), 0, s.main, b.groups,
+    hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,
                        !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
