@@ -183,7 +183,7 @@ def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0
     return jobs, expect, key_of
 
 
-def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, steps=64, warmup=16):
+def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, steps=64, warmup=16, settle_s=0.6):
     """config 4 with mainnet-shaped signing roots (one per 128-set committee):
     the same streaming window as the headline; k_prep hashes each distinct root of a call
     once (bgv_dslot.hsrc), so per-set work drops by most of hash_to_G2."""
@@ -199,17 +199,19 @@ def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, ste
             raise native.DeviceError(native.strerror(rc))
         return list(out), st
 
-    bcalls = super_batch_calls(steps, nsets, int(os.environ.get("BGV_DISPATCHERS", "2")))
+    bcalls = super_batch_calls(nsets)
+    ncalls = timed_calls(steps, bcalls, int(os.environ.get("BGV_DISPATCHERS", "2")))
     warm_calls = -(-warmup // bcalls) * bcalls
     ctx.set_batching(bcalls * nsets, 200000, 200000)
     try:
-        win = stream_window(step, expect, warm_calls, steps, 3 * bcalls)
+        win = stream_window(step, expect, warm_calls, ncalls, 3 * bcalls, settle_s=settle_s, boundary=bcalls)
     finally:
         ctx.set_batching(*default_batching())
     return {"config": "config4 with one signing root per %d sets (%d distinct roots + the corrupted-message "
-                      "ones per %d-set batch), %d steps after %d warmup, super-batches of %d calls"
-                      % (committee, -(-nsets // committee), nsets, steps, warm_calls, bcalls),
-            "value": nsets * steps / win["elapsed"], "unit": "sets/s"}
+                      "ones per %d-set batch), %d calls timed after %d warmup calls and >= %.1f s of full load, "
+                      "super-batches of %d calls"
+                      % (committee, -(-nsets // committee), nsets, ncalls, win["warm_calls"], settle_s, bcalls),
+            "value": nsets * ncalls / win["elapsed"], "unit": "sets/s"}
 
 
 def make_block_import(ctx, native, nkeys):
@@ -256,7 +258,7 @@ def block_import_latency(ctx, native, nkeys, runs=100):
             "runs": runs}
 
 
-def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
+def aggregate_throughput(ctx, native, nkeys, calls=2520, inflight=126, settle_s=0.6):
     """config 2: 1024 aggregate sets x 128 distinct cached keys (contiguous committees),
     distinct signing roots, all valid, sent as the pool sends them (8 batchable jobs of
     128 sets, index.ts:155-166); `calls` such calls streaming with `inflight` outstanding.
@@ -292,6 +294,7 @@ def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
     assert call(0) == [1] * len(jobs), "config-2 verdict mismatch"
     done.clear()
     ctx.set_batching(inflight * nsets, 20000, 20000)
+    t_begin = time.perf_counter()
     try:
         with ThreadPoolExecutor(max_workers=inflight) as pool:
             res = list(pool.map(call, range(calls)))
@@ -299,11 +302,14 @@ def aggregate_throughput(ctx, native, nkeys, calls=1512, inflight=126):
         ctx.set_batching(*default_batching())
     assert all(r == [1] * len(jobs) for r in res), "config-2 verdict mismatch"
     done.sort()
-    a, b = 2 * inflight - 1, len(done) - 1
+    b = len(done) - 1
+    a = 2 * inflight - 1
+    while a + inflight < b and done[a] - t_begin < settle_s:
+        a += inflight
     rate = nsets * (b - a) / (done[b] - done[a])
     return {"config": "config2: 1024 aggregate sets x 128 cached keys (8 batchable jobs of 128 sets), %d calls "
-                      "streaming, %d in flight; rate between the 2nd and the last super-batch completion"
-                      % (calls, inflight),
+                      "streaming, %d in flight; rate between the super-batch completion %.2f s into the stream "
+                      "(>= %.1f s of full load) and the last" % (calls, inflight, done[a] - t_begin, settle_s),
             "value": rate, "unit": "sets/s", "pubkeys_per_s": rate * per,
             # HBM bytes of the pubkey gather: one 112-B cache entry (affine G1,
             # 28-bit Montgomery limbs) + one 4-B index per aggregated key
@@ -459,16 +465,23 @@ def cpu_baseline(jobs, key_of, expect, nsample, min_seconds):
                          host["cgroup_cpus"], dt, r / len(distinct))}
 
 
-def super_batch_calls(steps, nsets, dispatchers=2, max_slots=163840):
-    """Calls per super-batch: the largest b with b * nsets <= max_slots dividing the timed
-    step count into a multiple of `dispatchers` super-batches.  The library keeps one
-    super-batch in flight per dispatcher, so completions repeat with a period of
-    `dispatchers` batches: a window of whole periods measures the steady-state rate."""
-    best = 1
-    for b in range(1, max(1, max_slots // nsets) + 1):
-        if steps % b == 0 and (steps // b) % dispatchers == 0:
-            best = b
-    return best
+def super_batch_calls(nsets, max_slots=None):
+    """Calls per super-batch: as many nsets-set calls as the library's default super-batch
+    geometry holds (BGV_MAX_BATCH_SLOTS, 131,072 slots: 16 calls of 8192 sets), whatever the
+    step count -- the bench measures the geometry the library ships."""
+    if max_slots is None:
+        max_slots = default_batching()[0]
+    return max(1, max_slots // nsets)
+
+
+def timed_calls(steps, bcalls, dispatchers=2):
+    """Calls inside the timed window: the requested steps rounded up to whole completion
+    periods.  Calls of one super-batch complete together and the library keeps one super-batch
+    in flight per dispatcher, so completions repeat with a period of bcalls * dispatchers calls;
+    a window that ends inside a burst would count calls whose device time it does not hold.
+    steps a multiple of the period (64 at the default geometry) are timed exactly."""
+    period = bcalls * dispatchers
+    return -(-steps // period) * period
 
 
 def stream_window(step, expect, warmup, steps, inflight, settle_s=0.0, boundary=1):
@@ -636,8 +649,8 @@ def main():
                     help="untimed full-load seconds before the window (on top of --warmup calls) so the window runs "
                          "at the power-settled clock; 0 disables")
     ap.add_argument("--calls-per-batch", type=int, default=0,
-                    help="calls merged per device super-batch (default: the largest divisor of --steps "
-                         "with <= 163840 sets)")
+                    help="calls merged per device super-batch (default: the library's default geometry, "
+                         "BGV_MAX_BATCH_SLOTS // --nsets = 16 calls of 8192 sets)")
     ap.add_argument("--no-epoch-sweep", action="store_true", help="skip the config-5 sweep leg")
     ap.add_argument("--check-ranks", action="store_true",
                     help="preflight: start the ranks, join the process group, print one line naming the ranks "
@@ -689,7 +702,8 @@ def main():
     # (W+K)-th completions both fall on super-batch boundaries, and a long coalescing window
     # so every super-batch fills to B calls (restored after the timed region)
     ndisp = int(os.environ.get("BGV_DISPATCHERS", "2"))
-    bcalls = args.calls_per_batch or super_batch_calls(args.steps, args.nsets, ndisp)
+    bcalls = args.calls_per_batch or super_batch_calls(args.nsets)
+    ncalls = timed_calls(args.steps, bcalls, ndisp)
     # the window opens on a super-batch boundary: at least `warmup` calls complete before it,
     # and at least --settle-s seconds of full load (the device's clock settles at its power
     # limit within ~0.3 s; a window inside that boost phase reads up to ~20 % high,
@@ -699,7 +713,7 @@ def main():
     ctx.profile(1)
     barrier()
     cuda_sync()
-    win = stream_window(step, expect, warm_calls, args.steps, max(args.inflight, 3 * bcalls),
+    win = stream_window(step, expect, warm_calls, ncalls, max(args.inflight, 3 * bcalls),
                         settle_s=args.settle_s, boundary=bcalls)
     warm_calls = win["warm_calls"]
     cuda_sync()
@@ -717,12 +731,12 @@ def main():
         block = block_import_latency(ctx, native, args.nkeys)
     mainnet = None
     if extras and args.nkeys >= 131072:
-        agg = aggregate_throughput(ctx, native, args.nkeys)
-        mainnet = mainnet_shaped_throughput(ctx, native, args.nkeys)
+        agg = aggregate_throughput(ctx, native, args.nkeys, settle_s=args.settle_s)
+        mainnet = mainnet_shaped_throughput(ctx, native, args.nkeys, settle_s=args.settle_s)
     sweep = None if args.no_epoch_sweep else epoch_sweep(ctx, native, barrier, rank, world)
 
     if rank == 0:
-        total_sets = args.nsets * args.steps * world
+        total_sets = args.nsets * ncalls * world
         opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["fp_mul_eq"]
         per_set = {"k_prep": opc["k_sig"] + opc["k_hash"] + opc["k_pk[n_pk=1]"], "k_miller": opc["k_miller"]}
         # timed region: HIP-event time per launch (a kernel's span includes its overlap with
@@ -734,7 +748,7 @@ def main():
         per_group = opc["k_final[per group]"] + opc["k_final[group sig pair]"]
         per_slot_close = opc["k_final[per product step]"] + opc["k_final[per slot sig add]"]
         pipeline_macs = ((sum(per_set.values()) + per_slot_close) * slots + per_group * groups) \
-            * MACS_PER_FP_MUL * args.steps * world
+            * MACS_PER_FP_MUL * ncalls * world
         pipeline_frac = pipeline_macs / elapsed / (PEAK_MAC_PER_S * world)
         # dominant kernel at full occupancy, alone on the device (roofline_isolated): its
         # algorithmic MACs (set pairs + the group pairs on the same launch) / its HIP-event time
@@ -762,7 +776,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / args.steps,
+            "ms_per_step": 1e3 * elapsed / ncalls,
+            "timed_steps": ncalls,
             "p50_batch_latency_ms": 1e3 * statistics.median(lat),
             "p50_batch_latency_ms_unloaded": 1e3 * statistics.median(lat1),
             "higher_is_better": True,
@@ -776,12 +791,13 @@ def main():
                        "batches_in_flight": max(args.inflight, 3 * bcalls), "calls_per_super_batch": bcalls,
                        "parallelism": "dp%d (independent batches per GPU)" % world},
             "timing": "steady state: calls stream with the given number in flight; the window runs from the "
-                      "%d-th to the %d-th completed call (exactly %d calls inside; the %d warmup steps are the "
-                      "first %d completions, rounded up to whole super-batches and extended to >= %.1f s of "
-                      "full load so the window runs at the power-settled clock), super-batches of %d calls so both "
-                      "edges fall on batch boundaries; %d calls completed in all"
-                      % (warm_calls, warm_calls + args.steps, args.steps, args.warmup, warm_calls, args.settle_s,
-                         bcalls, win["calls_total"]),
+                      "%d-th to the %d-th completed call (exactly %d calls inside: the %d requested steps rounded "
+                      "up to whole completion periods of %d dispatchers x %d-call super-batches, the library's "
+                      "default geometry, so both edges fall on batch boundaries; the %d warmup steps are the first "
+                      "%d completions, rounded up to whole super-batches and extended to >= %.1f s of full load so "
+                      "the window runs at the power-settled clock); %d calls completed in all"
+                      % (warm_calls, warm_calls + ncalls, ncalls, args.steps, ndisp, bcalls, args.warmup, warm_calls,
+                         args.settle_s, win["calls_total"]),
             "kernel_ms_per_launch": avg,
             "retries_per_step": statistics.mean(s.batch_retries for s in stats),
             "call_device_ms": statistics.mean(s.device_ms for s in stats),

@@ -96,7 +96,7 @@ static size_t idle_coalesce_us() {
 #define BGV_SPLIT_MIN_SETS 4096
 static size_t split_min_env() {
   static const size_t v = env_size("BGV_SPLIT_MIN", BGV_SPLIT_MIN_SETS, 0);
-  return v;
+  return v == 1 ? 2 : v;  // a one-set job is never cut (bgv_set_split)
 }
 static int dispatchers_per_device() {
   static const int v = (int)env_size("BGV_DISPATCHERS", BGV_DISPATCHERS, 1);
@@ -454,7 +454,10 @@ struct bgv_ctx {
   std::atomic<int> running{0};  // super-batches being run by dispatchers
   // calls of at least this many sets are spread over the devices (verify_split; 0: never)
   std::atomic<uint32_t> split_min{BGV_SPLIT_MIN_SETS};
-  std::atomic<int> split_inflight{0};  // asynchronous split calls not yet done (bgv_close waits)
+  // split calls not yet done (bgv_close waits for them); split_closing, set by bgv_close under
+  // split_mu before it waits, turns later split calls away.  Both under split_mu.
+  int split_inflight = 0;
+  bool split_closing = false;
   std::mutex split_mu;
   std::condition_variable split_cv;
   double kernel_ms[BGV_NKERNELS] = {};
@@ -661,6 +664,32 @@ static void call_fail(Call* call, int rc) {
   call_finish(call);
 }
 
+// The argument checks the reference raises before any crypto, for one job: *code = 2 when the
+// job goes to the device, else its verdict (empty job, empty aggregate, an index that is not
+// in the cache -- the first such set in set order).  -BGV_E_ARG for a malformed set record.
+// The caller holds cache_mu (shared).
+static int host_job_code(const bgv_ctx* c, const bgv_job& jb, const bgv_set* sets, int32_t* code) {
+  *code = 2;
+  if (jb.n_sets == 0) {
+    *code = -BGV_E_EMPTY_SET;
+    return BGV_OK;
+  }
+  for (uint32_t k = 0; k < jb.n_sets && *code == 2; ++k) {
+    const bgv_set& s = sets[jb.first_set + k];
+    if (s.n_pk == 0)
+      *code = -BGV_E_EMPTY_AGGREGATE;
+    else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes))
+      return -BGV_E_ARG;
+    else if (s.pk_indices)
+      for (uint32_t q = 0; q < s.n_pk; ++q)
+        if (s.pk_indices[q] >= c->n_pubkeys || (!c->bad_pk.empty() && c->bad_pk.count(s.pk_indices[q]))) {
+          *code = -BGV_E_BAD_INDEX;
+          break;
+        }
+  }
+  return BGV_OK;
+}
+
 // host-side checks and layout, on the caller's thread
 static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets,
                        int mode, int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user, int dev = -1) {
@@ -681,27 +710,9 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   call->code.assign(njobs, 2);
   {
     std::shared_lock<std::shared_mutex> clk(c->cache_mu);
-    // argument checks the reference raises before any crypto
     for (size_t j = 0; j < njobs; ++j) {
-      const bgv_job& jb = jobs[j];
-      if ((size_t)jb.first_set + jb.n_sets > nsets) return -BGV_E_ARG;
-      if (jb.n_sets == 0) {
-        call->code[j] = -BGV_E_EMPTY_SET;
-        continue;
-      }
-      for (uint32_t k = 0; k < jb.n_sets && call->code[j] == 2; ++k) {
-        const bgv_set& s = sets[jb.first_set + k];
-        if (s.n_pk == 0)
-          call->code[j] = -BGV_E_EMPTY_AGGREGATE;
-        else if (!s.msg || (!s.sig && s.sig_len) || (!s.pk_indices && !s.pk_bytes))
-          return -BGV_E_ARG;
-        else if (s.pk_indices)
-          for (uint32_t q = 0; q < s.n_pk; ++q)
-            if (s.pk_indices[q] >= c->n_pubkeys || (!c->bad_pk.empty() && c->bad_pk.count(s.pk_indices[q]))) {
-              call->code[j] = -BGV_E_BAD_INDEX;
-              break;
-            }
-      }
+      if ((size_t)jobs[j].first_set + jobs[j].n_sets > nsets) return -BGV_E_ARG;
+      if (host_job_code(c, jobs[j], sets, &call->code[j]) != BGV_OK) return -BGV_E_ARG;
     }
   }
   // pass-1 layout: non-batchable jobs own their groups; batchable jobs (worker mode) share
@@ -1568,7 +1579,8 @@ int bgv_close(bgv_ctx* c) {
   {
     // asynchronous split calls finish first: their pieces need the dispatchers
     std::unique_lock<std::mutex> lk(c->split_mu);
-    c->split_cv.wait(lk, [c] { return c->split_inflight.load() == 0; });
+    c->split_closing = true;
+    c->split_cv.wait(lk, [c] { return c->split_inflight == 0; });
   }
   {
     std::lock_guard<std::mutex> lk(c->qmu);
@@ -1670,7 +1682,9 @@ int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, i
     std::lock_guard<std::mutex> ulk(c->util_mu);
     for (size_t di = 0; di < c->devs.size(); ++di) {
       Device& d = c->devs[di];
-      if (hipSetDevice(d.id) != hipSuccess || hipMalloc(&staged[di], esz * n) != hipSuccess) {
+      // zeroed: k_cache_put writes no entry for an undecodable record
+      if (hipSetDevice(d.id) != hipSuccess || hipMalloc(&staged[di], esz * n) != hipSuccess ||
+          hipMemsetAsync(staged[di], 0, esz * n, d.stream) != hipSuccess) {
         free_staged();
         return -BGV_E_DEVICE;
       }
@@ -1744,6 +1758,20 @@ int bgv_pubkeys_put(bgv_ctx* c, uint32_t first, const uint8_t* keys, size_t n, i
     } else {
       std::lock_guard<std::mutex> ulk(c->util_mu);
       rc = cache_reserve(c, need);
+      // an undecodable record that overwrites an existing entry keeps the old entry: a call
+      // that passed its index check before this put may still read it (later calls reject
+      // the index with BGV_E_BAD_INDEX)
+      const uint32_t old_n = (uint32_t)c->n_pubkeys.load();
+      for (size_t di = 0; rc == BGV_OK && di < c->devs.size(); ++di) {
+        Device& d = c->devs[di];
+        if (hipSetDevice(d.id) != hipSuccess) rc = -BGV_E_DEVICE;
+        for (uint32_t i : bad)
+          if (rc == BGV_OK && i < old_n &&
+              hipMemcpyAsync(static_cast<uint8_t*>(staged[di]) + esz * (i - first),
+                             reinterpret_cast<const uint8_t*>(d.cache) + esz * i, esz, hipMemcpyDeviceToDevice,
+                             d.stream) != hipSuccess)
+            rc = -BGV_E_DEVICE;
+      }
       if (rc == BGV_OK) rc = copy_in();
       if (rc == BGV_OK) {
         for (uint32_t i = first; i < need; ++i) c->bad_pk.erase(i);  // overwritten entries
@@ -1792,6 +1820,23 @@ static bool split_wanted(const bgv_ctx* c, size_t nsets) {
   return c->devs.size() > 1 && split_min_sets(c) > 0 && nsets >= split_min_sets(c);
 }
 
+// A split call registers itself before it submits anything (false: the context is closing)
+// and deregisters when it no longer touches the context; bgv_close waits for the count to
+// drop to zero.  The notify happens under split_mu, so a woken bgv_close (and the
+// bgv_destroy after it) cannot free the context before split_leave has returned.
+static bool split_enter(bgv_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->split_mu);
+  if (c->split_closing) return false;
+  ++c->split_inflight;
+  return true;
+}
+
+static void split_leave(bgv_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->split_mu);
+  --c->split_inflight;
+  c->split_cv.notify_all();
+}
+
 static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets, int mode,
                         int32_t* out, bgv_stats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -1815,8 +1860,17 @@ static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv
   std::vector<std::unique_ptr<Child>> kids;
   std::vector<size_t> small;
   size_t small_sets = 0;
+  // a big job's host-side checks run on the whole job before it is cut, so they take
+  // precedence over every shard's device statuses, as in the unsplit call (job_precheck)
+  std::vector<int32_t> pre(njobs, 2);
+  {
+    std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+    for (size_t j = 0; j < njobs; ++j) {
+      if ((size_t)jobs[j].first_set + jobs[j].n_sets > nsets) return -BGV_E_ARG;
+      if (jobs[j].n_sets >= big && host_job_code(c, jobs[j], sets, &pre[j]) != BGV_OK) return -BGV_E_ARG;
+    }
+  }
   for (size_t j = 0; j < njobs; ++j) {
-    if ((size_t)jobs[j].first_set + jobs[j].n_sets > nsets) return -BGV_E_ARG;
     if (jobs[j].n_sets >= big) continue;
     small.push_back(j);
     small_sets += jobs[j].n_sets;
@@ -1849,7 +1903,7 @@ static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv
   // big jobs: one run of sets per device
   for (size_t j = 0; j < njobs; ++j) {
     const uint32_t n = jobs[j].n_sets;
-    if (n < big) continue;
+    if (n < big || pre[j] != 2) continue;
     for (size_t d = 0; d < K; ++d) {
       const size_t lo = n * d / K, hi = n * (d + 1) / K;
       if (hi <= lo) continue;
@@ -1879,6 +1933,10 @@ static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv
   }
   for (size_t j = 0; j < njobs; ++j) {
     if (jobs[j].n_sets < big) continue;
+    if (pre[j] != 2) {
+      out[j] = pre[j];
+      continue;
+    }
     int32_t code = 0;
     bool decided = false;
     std::vector<uint8_t> parts;
@@ -1911,7 +1969,9 @@ static int verify_split(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv
 
 int bgv_set_split(bgv_ctx* c, uint32_t min_sets) {
   if (!c) return -BGV_E_ARG;
-  c->split_min = min_sets;
+  // at least 2: a one-set job is never cut (its infinity-key verdict is false, not
+  // BLST_PK_IS_INFINITY, which a shard's codes cannot tell apart)
+  c->split_min = min_sets == 1 ? 2 : min_sets;
   return BGV_OK;
 }
 
@@ -1922,7 +1982,10 @@ int bgv_verify(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_set* set
     if (c->closed) return -BGV_E_CLOSED;
     if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
     if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
-    return verify_split(c, jobs, njobs, sets, nsets, mode, out, stats);
+    if (!split_enter(c)) return -BGV_E_CLOSED;
+    const int rc = verify_split(c, jobs, njobs, sets, nsets, mode, out, stats);
+    split_leave(c);
+    return rc;
   }
   Call* call = new Call();
   int rc = call_submit(c, call, jobs, njobs, sets, nsets, mode, out, stats, nullptr, nullptr);
@@ -1944,15 +2007,11 @@ int bgv_verify_async(bgv_ctx* c, const bgv_job* jobs, size_t njobs, const bgv_se
     if (c->closed) return -BGV_E_CLOSED;
     if ((njobs && (!jobs || !out)) || (nsets && !sets)) return -BGV_E_ARG;
     if (mode != BGV_MODE_WORKER && mode != BGV_MODE_PER_JOB) return -BGV_E_ARG;
-    c->split_inflight.fetch_add(1);
+    if (!split_enter(c)) return -BGV_E_CLOSED;
     std::thread([=] {
       const int rc = verify_split(c, jobs, njobs, sets, nsets, mode, out, stats);
       if (done) done(user, rc);
-      {
-        std::lock_guard<std::mutex> lk(c->split_mu);
-        c->split_inflight.fetch_sub(1);
-      }
-      c->split_cv.notify_all();
+      split_leave(c);
     }).detach();
     return BGV_OK;
   }

@@ -29,12 +29,8 @@
 #ifdef BGV_BULK_MILLER_INLINE
 #define BGV_LAZY_INLINE_MUL 1
 #endif
-// -DBGV_BULK_MILLER_ASM: the products of this unit go to the hand-scheduled subroutines
-// (bgv_fpmul_asm.h) through exact-clobber calls instead of the ABI calls to fp_mul_l.  Measured
-// equal at the kernel level (profiles/r04/asm_ab: k_miller 10.69-10.76 vs 10.71-10.86 ms), so off.
-#if defined(BGV_BULK_MILLER_ASM) && !defined(BGV_ASM_MUL)
-#define BGV_ASM_MUL 1
-#endif
+// (Hand-scheduled exact-clobber product subroutines measured equal at the kernel level,
+// profiles/r04/asm_ab: k_miller 10.69-10.76 vs 10.71-10.86 ms; kept in tools/experimental/.)
 #include "bgv_device.h"
 
 #ifndef BGV_WPE_LINES

@@ -16,7 +16,6 @@
 #include "bgv_tcurve.h"
 #include "bgv_tg1.h"
 #include "bgv_tround_dev.h"
-#include "bgv_wround.h"
 
 static __constant__ uint8_t kTcProg[TCP_TABLE_BYTES] = TCP_TABLE_INIT;
 static __constant__ uint8_t kTg1Prog[TG1_TABLE_BYTES] = TG1_TABLE_INIT;
@@ -377,95 +376,6 @@ __global__ void __launch_bounds__(64) k_prep_wide(const bgv_dslot* __restrict__ 
   }
 }
 
-// k_prep_wide on four waves per set and task (bgv_wround.h tc_wave4_engine: each real
-// instruction of a round on one wave with the limbs spread over its lanes, the block's four
-// waves one per SIMD): the same schedules, formulas and slot values as k_prep_wide, a round in
-// the time of its longest wave's one or two instructions.  Plane 3 (the pubkey task) runs on
-// the first wave only.
-__global__ void __launch_bounds__(256) k_prep_wide4(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                                    g2_jac* __restrict__ h, fp12_t* __restrict__ f,
-                                                    g2_jac* __restrict__ rsig, int32_t* __restrict__ sig_status,
-                                                    const uint32_t* __restrict__ pk_idx,
-                                                    const g1_aff* __restrict__ cache, const uint8_t* __restrict__ pk_bytes,
-                                                    g1_jac* __restrict__ rpk, int32_t* __restrict__ pk_status,
-                                                    g1_jac* __restrict__ pk_agg) {
-  __shared__ uint8_t prog[TCP_TABLE_BYTES];
-  __shared__ fp_t S[TCP_NSLOT];
-  __shared__ int flag;
-  const int t = threadIdx.x;
-  if (blockIdx.y == 3) {
-    if (t >= 64) return;  // one wave: the tree (cross-lane within the wave) and lane 0's task
-    const uint32_t s = blockIdx.x;
-    if (pk_agg) pk_agg_one(slots, s, pk_idx, cache, pk_agg);
-    if (t == 0) task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
-    return;
-  }
-  const uint32_t uu = blockIdx.x;  // grid = exactly nslots blocks per task
-  const bgv_dslot& d = slots[uu];
-  const bool real = !(d.flags & BGV_SLOT_PAD);
-  if (blockIdx.y == 2 && (!real || sig_status[uu] != BGV_ST_OK)) return;  // block-uniform
-  for (int i = t; i < TCP_TABLE_BYTES; i += 256) prog[i] = kTcProg[i];
-  if (t == 6) {
-    S[TCP_S_ONE] = fp_one();
-  } else if (t >= 7 && t < 11) {
-    const fp2_t cx = BGV_PSI_CX, cy = BGV_PSI_CY;
-    const fp2_t& v = t < 9 ? cx : cy;
-    S[t < 9 ? TCP_S_PSI_CX + (t - 7) : TCP_S_PSI_CY + (t - 9)] = (t & 1) ? v.c0 : v.c1;
-  } else if (t == 11) {
-    S[TCP_S_PSI2_CX] = fp_t{BGV_PSI2_CX};
-  } else if (t == 12) {
-    S[TCP_S_PSI2_CY] = fp_t{BGV_PSI2_CY};
-  }
-  for (int i = t; i < TC_ISO_NCONST; i += 256) S[TCP_S_ISO + i] = tc_iso_const(i);
-  tc_wave4_engine e{prog, S, wr_init(), t / 64, false};
-  if (blockIdx.y == 0) {
-    if (t < 6) {
-      S[TCP_BANK(1) + t] = reinterpret_cast<const fp_t*>(h + uu)[t];
-      S[TCP_BANK(2) + t] = reinterpret_cast<const fp_t*>(split_q1(f, uu))[t];
-    }
-    __syncthreads();
-    tc_clear_cofactor(e);
-    if (t == 0) flag = e.bad ? 1 : 0;
-    __syncthreads();
-    if (real) {
-      if (!flag) {
-        if (t < 6) reinterpret_cast<fp_t*>(h + uu)[t] = S[TCP_BANK(3) + t];
-      } else if (t == 0) {
-        h[uu] = g2_clear_cofactor(jac_add(iso_map_g2_jac(h[uu]), iso_map_g2_jac(*split_q1(f, uu))));
-      }
-    }
-  } else if (blockIdx.y == 1) {
-    const bool ok = sig_status[uu] == BGV_ST_OK;  // read before the subgroup blocks may flip it
-    if (t < 4)
-      S[TCP_BANK(1) + t] = reinterpret_cast<const fp_t*>(split_sig(f, uu))[t];
-    else if (t < 6)
-      S[TCP_BANK(1) + t] = t == 4 ? fp_one() : fp_zero();
-    __syncthreads();
-    tc_mul_glv(e, d.scalar);
-    if (real && ok && t < 6) reinterpret_cast<fp_t*>(rsig + uu)[t] = S[TCP_BANK(4) + t];
-  } else {
-    if (t < 6) {
-      const fp_t v = t < 4 ? reinterpret_cast<const fp_t*>(split_sig(f, uu))[t] : (t == 4 ? fp_one() : fp_zero());
-      S[TCP_BANK(0) + t] = v;
-      S[TCP_BANK(4) + t] = v;
-    }
-    __syncthreads();
-    const int a = tc_to_jac(e, tc_mul_x_abs(e));
-    if (t == 0) {
-      const g2_jac p = jac_from_aff(*split_sig(f, uu));
-      bool in;
-      if (e.bad) {
-        in = g2_in_subgroup(p);
-      } else {
-        const fp_t* B = S + TCP_BANK(a);
-        const g2_jac xp = {{B[0], B[1]}, {B[2], B[3]}, {B[4], B[5]}};
-        in = jac_eq(g2_psi(p), jac_neg(xp));  // psi(P) == [x]P = -[|x|]P
-      }
-      if (!in) sig_status[uu] = BGV_POINT_NOT_IN_GROUP;
-    }
-  }
-}
-
 // Committee-sized sets (BGV_PK_TREE_MIN..BGV_PK_TEAM_MAX cached keys, e.g. 128-key
 // attestation aggregates) on a team of 16 lanes, four sets per wave: lane l sums keys
 // l, l + 16, ... with mixed additions, then four ds_swizzle butterfly levels (xor 8..1, inside
@@ -507,16 +417,8 @@ hipError_t bgv_launch_prep(const bgv_dev_batch& b, const bgv_streams& s) {
     const g1_aff* cache = reinterpret_cast<const g1_aff*>(b.cache_opaque);
     const hipError_t e = bgv_launch_prep_wave(b, s.main);
     if (e != hipSuccess) return e;
-    static const bool four = [] {  // BGV_WIDE4=1: the four-wave engine (bgv_wround.h)
-      const char* e = getenv("BGV_WIDE4");
-      return e && *e == '1';
-    }();
-    if (four)
-      hipLaunchKernelGGL(k_prep_wide4, dim3(n, 4), dim3(256), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
-                         b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
-    else
-      hipLaunchKernelGGL(k_prep_wide, dim3(n, 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
-                         b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
+    hipLaunchKernelGGL(k_prep_wide, dim3(n, 4), dim3(64), 0, s.main, b.slots, n, b.h, b.f, b.rsig, b.sig_status,
+                       b.pk_idx, cache, b.pk_bytes, b.rpk, b.pk_status, tree ? b.pk_agg : nullptr);
     BGV_MARK(1);
     return hipGetLastError();
   }

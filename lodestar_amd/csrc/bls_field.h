@@ -275,23 +275,10 @@ BGV_MUL_ATTR fp_t fp_sqr_l(BGV_U14(a_)) {
   return fp_sqr_body(a);
 }
 
-// BGV_ASM_MUL (device code): the products go to the hand-scheduled subroutines of
-// bgv_fpmul_asm.h (tools/gen_fpmul_asm.py) through inline-asm calls with an exact clobber set
-// instead of the ABI calls to fp_mul_l / fp_sqr_l: same limbs, bit for bit.
-#include "bgv_fpmul_asm.h"
-#if defined(__HIP_DEVICE_COMPILE__) && defined(BGV_ASM_MUL)
-#define BGV_USE_ASM_MUL 1
-__device__ __forceinline__ fp_t fp_mul(const fp_t& a, const fp_t& b) {
-  fp_t r = a;
-  bgv_fpmul_asm(r.v, b);
-  return r;
-}
-__device__ __forceinline__ fp_t fp_sqr(const fp_t& a) {
-  fp_t r = a;
-  bgv_fpsqr_asm(r.v);
-  return r;
-}
-#elif defined(__HIP_DEVICE_COMPILE__) && defined(BGV_WAVE_UNIFORM_MUL)
+// (A hand-scheduled product subroutine with an exact clobber set, tools/experimental/
+// bgv_fpmul_asm.h, measured equal to the ABI call at the kernel level in round 4 and is not
+// part of the library.)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BGV_WAVE_UNIFORM_MUL)
 // BGV_WAVE_UNIFORM_MUL (device code of a unit whose kernels run one set per wave, every lane
 // holding the same values): each product on the whole wave (bgv_wfp.h wfp_umul, defined there).
 __device__ __noinline__ fp_t wfp_umul_l(BGV_U14(a_), BGV_U14(b_));

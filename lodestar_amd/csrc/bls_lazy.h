@@ -194,8 +194,6 @@ BGV_HD lzr lz_mul(const lz<LA, VA>& a, const lz<LB, VB>& b) {
 #if defined(BGV_LAZY_INLINE_MUL)
   BGV_COUNT_MUL();
   const fp_t r = fp_mul_body(fp_t{{BGV_V14(a)}}, fp_t{{BGV_V14(b)}});
-#elif defined(BGV_USE_ASM_MUL)
-  const fp_t r = fp_mul(fp_t{{BGV_V14(a)}}, fp_t{{BGV_V14(b)}});
 #else
   const fp_t r = fp_mul_l(BGV_V14(a), BGV_V14(b));
 #endif
@@ -213,8 +211,6 @@ BGV_HD lzr lz_sqr(const lz<LA, VA>& a) {
 #if defined(BGV_LAZY_INLINE_MUL)
   BGV_COUNT_SQR();
   const fp_t r = fp_sqr_body(fp_t{{BGV_V14(a)}});
-#elif defined(BGV_USE_ASM_MUL)
-  const fp_t r = fp_sqr(fp_t{{BGV_V14(a)}});
 #else
   const fp_t r = fp_sqr_l(BGV_V14(a));
 #endif

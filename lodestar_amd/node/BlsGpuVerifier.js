@@ -35,8 +35,28 @@ const MAX_BUFFERED_SIGS = 63;
 const MAX_BUFFER_WAIT_MS = 1;
 
 const SignatureSetType = {single: "single", aggregate: "aggregate"};
-const BGV_E_ARG = 23; // include/blsgpu.h
 const PUBKEY_RUN = 8192;
+// include/blsgpu.h: BGV_BLST_* decode statuses are 1..19 (library codes start at 20)
+const isBlstDecodeCode = (code) => typeof code === "number" && code <= -1 && code >= -19;
+
+// One contiguous run of queued validator keys: indices [first, first + n), their 48-byte
+// encodings packed in order into bytes (capacity doubles up to PUBKEY_RUN keys).
+class PubkeyRun {
+  constructor(first) {
+    this.first = first;
+    this.n = 0;
+    this.bytes = new Uint8Array(48 * 64);
+  }
+  push(pubkey) {
+    if (48 * (this.n + 1) > this.bytes.length) {
+      const b = new Uint8Array(Math.min(2 * this.bytes.length, 48 * PUBKEY_RUN));
+      b.set(this.bytes.subarray(0, 48 * this.n));
+      this.bytes = b;
+    }
+    this.bytes.set(pubkey, 48 * this.n);
+    this.n++;
+  }
+}
 
 class QueueError extends Error {
   constructor(code) {
@@ -91,7 +111,8 @@ class BlsGpuVerifier {
   constructor(opts = {}, modules = {}) {
     this.metrics = modules.metrics || null;
     this.ctx = opts.ctx || addon.init(opts.devices || []);
-    this.pendingPubkeys = [];
+    this.pendingRuns = []; // PubkeyRun in hook order
+    this.pendingKeys = 0;
     this.flushing = null;
     this.onPubkeyError = opts.onPubkeyError || null;
     this.blsVerifyAllMultiThread = opts.blsVerifyAllMultiThread || false;
@@ -117,9 +138,17 @@ class BlsGpuVerifier {
   pubkeyAddedHook() {
     return (index, pubkey, pk) => {
       if (pk && typeof pk === "object") pk.index = index;
-      this.pendingPubkeys.push([index, pubkey]);
+      // packed into its run here, in the caller's time (the state transition adds keys one at a
+      // time), so a flush hands whole runs to the addon without touching each key again
+      let r = this.pendingRuns[this.pendingRuns.length - 1];
+      if (!r || r.first + r.n !== index || r.n >= PUBKEY_RUN) {
+        r = new PubkeyRun(index);
+        this.pendingRuns.push(r);
+      }
+      r.push(pubkey);
+      this.pendingKeys++;
       // a gap error here reappears at the next verifySignatureSets, which awaits the flush
-      if (this.pendingPubkeys.length >= 65536) this.flushPubkeys().catch(() => {});
+      if (this.pendingKeys >= 65536) this.flushPubkeys().catch(() => {});
     };
   }
 
@@ -129,15 +158,18 @@ class BlsGpuVerifier {
    * waiting for running verifies), so a validator-set growth never stalls the event loop
    * (EpochContext.addPubkey, state-transition/src/cache/epochContext.ts:702-705;
    * pubkeyCache.ts:56-77).  One flush chain at a time; keys queued meanwhile join it.
-   * A run that fails for a gap in the indices (nothing written) stays queued, with every run
-   * after it, and the error reaches the caller.  A run with undecodable records is committed
-   * with those indices marked (sets naming them reject BGV_E_BAD_INDEX): it is reported once
-   * (onPubkeyError, else a console warning) and dropped, so one bad key cannot stop later
-   * uploads or verification.
+   * Only a run whose records fail to decode (a BLST status) is committed -- with those indices
+   * marked, so sets naming them reject BGV_E_BAD_INDEX -- then reported once (onPubkeyError,
+   * else a console warning) and dropped, so one bad key cannot stop later uploads or
+   * verification.  Any other failure (a gap in the indices, a device or memory error) wrote
+   * nothing: that run stays queued with every run after it, and the error reaches the caller.
+   * The runs are packed as the hook receives the keys, so the event loop only sorts a few run
+   * records here and hands the addon views of their bytes (the addon holds a reference to each
+   * until its put completes).
    */
   flushPubkeys() {
     if (this.closed) return Promise.resolve();
-    if (!this.flushing && this.pendingPubkeys.length) {
+    if (!this.flushing && this.pendingRuns.length) {
       this.flushing = this._flushRuns().finally(() => {
         this.flushing = null;
       });
@@ -146,31 +178,29 @@ class BlsGpuVerifier {
   }
 
   async _flushRuns() {
-    while (this.pendingPubkeys.length && !this.closed) {
-      const p = this.pendingPubkeys;
-      this.pendingPubkeys = [];
+    while (this.pendingRuns.length && !this.closed) {
+      const runs = this.pendingRuns;
+      this.pendingRuns = [];
+      this.pendingKeys = 0;
       let sorted = true;
-      for (let k = 1; k < p.length && sorted; k++) sorted = p[k][0] > p[k - 1][0];
-      if (!sorted) p.sort((a, b) => a[0] - b[0]);
+      for (let k = 1; k < runs.length && sorted; k++) sorted = runs[k].first > runs[k - 1].first;
+      if (!sorted) runs.sort((a, b) => a.first - b.first);
       let i = 0;
       try {
-        while (i < p.length) {
-          // contiguous runs of at most PUBKEY_RUN keys: the main thread only copies one run's
-          // bytes between awaits
-          let j = i + 1;
-          while (j < p.length && j - i < PUBKEY_RUN && p[j][0] === p[j - 1][0] + 1) j++;
-          const buf = new Uint8Array(48 * (j - i));
-          for (let k = i; k < j; k++) buf.set(p[k][1], 48 * (k - i));
+        for (; i < runs.length; i++) {
+          const r = runs[i];
           try {
-            await addon.pubkeysPutAsync(this.ctx, p[i][0], buf, 48);
+            await addon.pubkeysPutAsync(this.ctx, r.first, r.bytes.subarray(0, 48 * r.n), 48);
           } catch (e) {
-            if (e.bgvCode === -BGV_E_ARG || this.closed) throw e;
-            this.reportPubkeyError(e, p[i][0], j - i);
+            if (!isBlstDecodeCode(e.bgvCode) || this.closed) throw e;
+            this.reportPubkeyError(e, r.first, r.n);
           }
-          i = j;
         }
       } finally {
-        if (i < p.length) this.pendingPubkeys = p.slice(i).concat(this.pendingPubkeys);
+        if (i < runs.length) {
+          this.pendingRuns = runs.slice(i).concat(this.pendingRuns);
+          this.pendingKeys = this.pendingRuns.reduce((a, r) => a + r.n, 0);
+        }
       }
     }
   }
@@ -182,7 +212,7 @@ class BlsGpuVerifier {
   }
 
   async verifySignatureSets(sets, opts = {}) {
-    if (this.pendingPubkeys.length || this.flushing) await this.flushPubkeys();
+    if (this.pendingRuns.length || this.flushing) await this.flushPubkeys();
     const nAgg = getAggregatedPubkeysCount(sets);
     this.counters.aggregatedPubkeys += nAgg;
     if (this.metrics) this.metrics.bls.aggregatedPubkeys.inc(nAgg);

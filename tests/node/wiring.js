@@ -101,6 +101,7 @@ const impls = {BlsSingleThreadVerifier: FakeSingle, BlsMultiThreadWorkerPool: Fa
     // measured window is the upload that follows, with gossip-style calls in flight
     const first = 3;
     for (let i = 0; i < N; i++) hook(first + i, pks48.subarray(48 * i, 48 * i + 48), {});
+    if (global.gc) global.gc();  // the hook calls' garbage is the caller's (node --expose-gc)
     let last = process.hrtime.bigint();
     let maxGap = 0;
     const ticker = setInterval(() => {
@@ -119,9 +120,11 @@ const impls = {BlsSingleThreadVerifier: FakeSingle, BlsMultiThreadWorkerPool: Fa
     assert.strictEqual(sN, false, "the last added key is in the cache (wrong signature for it: false)");
     console.log(JSON.stringify({pubkey_upload: {keys: N, call_ms_p50: callMs, max_event_loop_gap_ms: maxGap}}));
     // a synchronous put of the same keys held the loop ~20 ms; the asynchronous one leaves
-    // only the gaps of the 64 calls' own packing and promise work (timer-based, so a bound
-    // with headroom: two calls' latency, at least 8 ms)
-    assert.ok(maxGap <= Math.max(2 * callMs, 8), `event loop stalled ${maxGap} ms (one call ${callMs} ms)`);
+    // only the gaps of the 64 calls' own packing and promise work.  r04's 5.15 ms gap was the
+    // flush copying 8192 keys per run one by one on the main thread (and checking the order of
+    // 65,536 entries): the hook now packs the keys into their runs, so the flush only hands
+    // views to the addon (tests/node/flush_mock.js measures it without a GPU: ~2 ms)
+    assert.ok(maxGap <= Math.max(callMs, 5), `event loop stalled ${maxGap} ms (one call ${callMs} ms)`);
     await v.close();
   }
   console.log("wiring ok");

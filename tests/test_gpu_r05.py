@@ -1,0 +1,89 @@
+"""GPU tests added in round 5.
+
+One call over several devices (bgv_set_split; advisor r04): a job big enough to be cut into
+per-device runs takes its host-side checks (an index not in the cache, an empty aggregate) on
+the whole job before it is cut, so they decide the job ahead of any device status -- an
+undecodable signature in an earlier run included -- exactly as in the unsplit call
+(bgv_api.cpp job_precheck; the reference raises them before any crypto:
+packages/beacon-node/src/chain/bls/maybeBatch.ts:16-39, chain/bls/utils.ts:5-16).  A one-set job
+is never cut (bgv_set_split(1) acts as 2).
+"""
+import hashlib
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+NKEYS = 8192
+
+
+def _sk(i):
+    return (int.from_bytes(hashlib.sha256(i.to_bytes(32, "little")).digest(), "little") % R).to_bytes(32, "big")
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    from lodestar_amd import native
+    sks = [_sk(i) for i in range(NKEYS)]
+    out = []
+    for devs in ([0], [0, 0]):
+        c = native.Context(devs)
+        c.keygen(b"".join(sks), cache_first=0, want_pubkeys=False)
+        out.append(c)
+    out[1].set_split(2048)
+    yield out, sks
+    for c in out:
+        c.close()
+
+
+def _sets(c, sks, n):
+    from lodestar_amd import native
+    roots = [hashlib.sha256(b"r05-split-%d" % i).digest() for i in range(n)]
+    sigs = c.sign(b"".join(sks[i] for i in range(n)), b"".join(roots))
+    return [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[i]) for i in range(n)]
+
+
+def test_split_host_checks_precede_device_statuses(ctxs):
+    from lodestar_amd import native
+    (one, two), sks = ctxs
+    base = _sets(one, sks, 4096)
+    broken = lambda s: native.SetSpec(s.msg, bytes([s.sig[0] & 0x7F]) + s.sig[1:], pk_indices=list(s.pk_indices))
+    # undecodable signature early (first device's run), index outside the cache late (second run)
+    sets = list(base)
+    sets[10] = broken(base[10])
+    sets[4000] = native.SetSpec(base[4000].msg, base[4000].sig, pk_indices=[NKEYS + 5])
+    got = [c.verify_jobs([(sets, False)], native.MODE_WORKER) for c in (one, two)]
+    assert got == [[-native.BGV_E_BAD_INDEX]] * 2
+    # an empty aggregate late beats the undecodable signature early too
+    sets[4000] = native.SetSpec(base[4000].msg, base[4000].sig, pk_indices=[])
+    got = [c.verify_jobs([(sets, False)], native.MODE_WORKER) for c in (one, two)]
+    assert got == [[-native.BGV_E_EMPTY_AGGREGATE]] * 2
+    # without a host-side condition the first undecodable signature in set order decides
+    sets[4000] = broken(base[4000])
+    got = [c.verify_jobs([(sets, False)], native.MODE_WORKER) for c in (one, two)]
+    assert got == [[-native.BLST_BAD_ENCODING]] * 2
+    # and the valid job, and a host-checked job beside small jobs of the same call
+    small = [([s], True) for s in base[:300]]
+    sets[10] = base[10]
+    sets[4000] = native.SetSpec(base[4000].msg, base[4000].sig, pk_indices=[NKEYS + 1])
+    for c in (one, two):
+        assert c.verify_jobs([(base, False)], native.MODE_WORKER) == [1]
+        codes = c.verify_jobs(small + [(sets, False)], native.MODE_WORKER)
+        assert codes == [1] * 300 + [-native.BGV_E_BAD_INDEX]
+
+
+def test_split_min_one_acts_as_two(ctxs):
+    from lodestar_amd import native
+    (one, two), sks = ctxs
+    base = _sets(one, sks, 3000)
+    wrong = native.SetSpec(base[1].msg, base[0].sig, pk_indices=[0])
+    jobs = [([s], True) for s in base] + [([wrong], True)]
+    try:
+        two.set_split(1)
+        want = one.verify_jobs(jobs, native.MODE_WORKER)
+        assert want == [1] * 3000 + [0]
+        assert two.verify_jobs(jobs, native.MODE_WORKER) == want
+        assert two.verify_jobs([([wrong], False)], native.MODE_WORKER) == [0]
+    finally:
+        two.set_split(2048)

@@ -10,7 +10,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "lodestar_amd", "csrc", "bgv_fpmul_asm.h")
+SRC = os.path.join(ROOT, "tools", "experimental", "bgv_fpmul_asm.h")
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 N0, M = 0xffcfffd, (1 << 28) - 1
 

@@ -1,4 +1,4 @@
-"""Generate lodestar_amd/csrc/bgv_fpmul_asm.h: the 28-bit-limb Montgomery product and square as
+"""Generate tools/experimental/bgv_fpmul_asm.h (an experiment kept out of the product library): the 28-bit-limb Montgomery product and square as
 hand-scheduled gfx950 subroutines with a register contract of their own.
 
     python tools/gen_fpmul_asm.py
@@ -26,7 +26,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "lodestar_amd", "csrc", "bgv_fpmul_asm.h")
+OUT = os.path.join(ROOT, "tools", "experimental", "bgv_fpmul_asm.h")
 
 P = [0xfffaaab, 0xfefffff, 0x3ffffb9, 0xfffeb15, 0x6241eab, 0xa0f6b0f, 0xf6730d2, 0xf38512b, 0x4774b84, 0x4bacd76,
      0xba7b643, 0xe69a4b1, 0x1ea397f, 0x001a011]

@@ -6,6 +6,8 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    python bench.py (the default command the driver runs)  -> OUTDIR/bench_default.json
 #   quick    bench headline window only (no CPU baseline, no extras) -> OUTDIR/bench_quick.jsonl (appends)
+#   driver   the headline window with the driver's step counts (--steps 20 --warmup 5) and with
+#            the default ones (64 / 16), back to back                 -> OUTDIR/bench_steps.jsonl (appends)
 #   trace    rocprofv3 --kernel-trace --stats of the bench command   -> OUTDIR/bench_trace/
 #   roof     rocprofv3 --kernel-trace --stats of the isolated roofline call -> OUTDIR/roof_trace/
 #   pmc      the PMC passes of the roofline call (tools/gpu/pmc.sh)  -> gpurun_out/<basename OUTDIR>/pmc
@@ -36,6 +38,13 @@ for step in "$@"; do
       timeout -k 10 150 python bench.py --no-cpu-baseline --no-block-import --no-epoch-sweep \
         >> "$O/bench_quick.jsonl" 2>> "$O/bench_quick.err" || fail quick $? "$O/bench_quick.err"
       tail -1 "$O/bench_quick.jsonl" | python tools/gpu/summarize.py - ;;
+    driver)
+      for sw in "20 5" "64 16"; do
+        read -r ks kw <<< "$sw"
+        timeout -k 10 150 python bench.py --steps $ks --warmup $kw --no-cpu-baseline --no-block-import --no-epoch-sweep \
+          >> "$O/bench_steps.jsonl" 2>> "$O/bench_steps.err" || fail driver $? "$O/bench_steps.err"
+      done
+      tail -2 "$O/bench_steps.jsonl" | python tools/gpu/summarize.py - ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/bench_trace" -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline > "$O/bench_traced.json" 2> "$O/bench_traced.err" \

@@ -23,7 +23,7 @@ for f in sys.argv[1:]:
             if k in d:
                 v = d[k].get("p50_latency_ms") if k == "block_import" else round(d[k]["value"] / 1e6, 3)
                 extra.append("%s %s" % (lbl, v))
-        print(name.split("/")[-1], "value %.3fM" % (d["value"] / 1e6), "p50", round(d["p50_batch_latency_ms"], 1),
+        print(name.split("/")[-1], "steps %s/%s" % (d.get("steps"), d.get("timed_steps")), "value %.3fM" % (d["value"] / 1e6), "p50", round(d["p50_batch_latency_ms"], 1),
               "frac", round(r["frac"], 3), r.get("kernel", ""), "iso",
               {k: round(v, 2) for k, v in r.get("kernel_ms_isolated", {}).items()},
               "pf", round(r["pipeline_frac"], 3), " ".join(extra), flush=True)

@@ -14,6 +14,7 @@
 
 #define BGV_ASM_EMIT 1
 #include "../lodestar_amd/csrc/bls_field.h"
+#include "experimental/bgv_fpmul_asm.h"
 
 #define CHECK(x)                                                                             \
   do {                                                                                       \

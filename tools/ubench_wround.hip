@@ -1,4 +1,4 @@
-// The wave round engine (lodestar_amd/csrc/bgv_wround.h) against the four-part engine
+// The wave round engine (tools/experimental/bgv_wround.h, not in the product library) against the four-part engine
 // (bgv_tround_dev.h) on the latency path's G2 point programs: [|x|]P and the cofactor clearing
 // for random points (one set per block), banks compared limb for limb, then the time of one
 // [|x|]P chain (63 doublings + 5 additions, 214 rounds) on each.
@@ -9,7 +9,7 @@
 #include <vector>
 
 #include "bgv_tround_dev.h"
-#include "bgv_wround.h"
+#include "experimental/bgv_wround.h"
 
 #define CHECK(x)                                                                \
   do {                                                                          \
