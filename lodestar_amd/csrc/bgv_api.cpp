@@ -112,6 +112,15 @@ static int execs_per_device() {
 // Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
 // retry rounds of several super-batches then run side by side instead of queueing behind one
 // another (their rounds are latency-bound chains of small launches)
+// BGV_FPW=0 turns off the first pass's weighted tests of its failing groups (run_pass1), for
+// A/B measurements; on by default
+static bool fpw_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("BGV_FPW");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
 static int retry_threads_per_device() {
   static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
   return v;
@@ -182,6 +191,11 @@ struct Exec {
   size_t pout_cap = 0;
   uint32_t* d_lines = nullptr;  // the bulk Miller loop's line records (bgv_lines_pairs)
   uint32_t lines_cap = 0;       // pairs
+  // the first pass's weighted tests (bgv_launch_fpw_*): [0] their count, [1 + i] test i's
+  // first-pass group; host mirror
+  uint32_t* d_fpw = nullptr;
+  size_t fpw_cap = 0;
+  Pinned<uint32_t> h_fpw;
 };
 
 // bgv_final_verify's device buffers (under util_mu)
@@ -358,19 +372,12 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // every invalid job is a candidate of that one pair); a failing single job is invalid; jobs of
 // a failing pair next to other failures are tested alone in one more round.
 //
-// Weighted test (kind 2, one-set jobs, bulk rounds): before any pattern test, ONE device group
-// over the whole unit in which slot k enters with weight k + 1 (bgv_layout.h
-// BGV_GROUP_WEIGHTED): its value is W = prod_k X_k^(k+1) against the first-pass value
-// V = prod_k X_k (X_k the slot's pairing value, 1 when valid).  With exactly one invalid slot k,
-// W = V^(k+1) and the closing finds w = k + 1 (the only w <= 64 with V^w = W: V has prime order
-// r); the invalid job is identified with one test instead of ceil(log2 n).  Two or more invalid
-// jobs match no w except with probability ~2^-50 over the randomizers (the same order as a
-// pattern test passing by accident); the unit then takes the pattern tests next round
-// (unit_rounds -1).  A failing group usually holds one invalid job (at 1 % corrupted sets, 72 %
-// of the failing 64-set groups), so most are resolved with one Miller loop and one closing.
+// A failing shared group of a bulk batch has already had ONE weighted test in the first pass
+// (run_pass1, bgv_launch_fpw_*): a group with exactly one invalid slot is decided there, so the
+// units that reach the retry rounds hold two or more invalid jobs (or were not testable).
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
-  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs; 2: weighted test
+  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs
   std::vector<size_t> jobs;        // kind 0: its jobs in slot order
   std::vector<uint32_t> tests;     // round group index of each test
   std::vector<std::vector<size_t>> test_jobs;  // kind 1: each test's jobs
@@ -399,7 +406,7 @@ struct Call {
   std::vector<int32_t> set_sig, set_pk;
   std::vector<std::vector<size_t>> units;  // pending retry units
   std::vector<int> unit_group;             // first-pass group the unit's jobs lie in (-1: not known)
-  std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through (-1: a weighted test)
+  std::vector<int> unit_rounds;            // pattern rounds the unit's jobs have been through
   std::vector<std::vector<uint32_t>> unit_idx;  // after a pattern round: the candidates' pattern indices
   std::vector<uint32_t> unit_dmask;        // ... and the index bits D of their pairing (0: none)
   std::vector<Part> parts;
@@ -443,10 +450,6 @@ struct bgv_ctx {
   // BGV_FAULT_INJECT=1 at bgv_init: every super-batch fails as a HIP error would (tests of
   // the device-error path: every job in flight rejects with BGV_E_DEVICE, none resolves false)
   bool fault_inject = false;
-  // BGV_WEIGHTED=1 at bgv_init: retry rounds start a failing group of one-set jobs with a
-  // weighted test (PatternUnit kind 2).  Off by default: it saves tests but adds a retry round,
-  // and at 1 % corrupted sets the bench measured 2.08 M vs 2.40 M sets/s (profiles/r04/weighted_ab/).
-  bool weighted = false;
   // super-batch geometry (bgv_set_batching; env defaults at bgv_init)
   std::atomic<uint32_t> max_slots{BGV_MAX_BATCH_SLOTS};
   std::atomic<uint32_t> coalesce{BGV_COALESCE_US};
@@ -571,8 +574,8 @@ static int exec_create(Exec* x) {
 
 static void exec_destroy(Exec* x) {
   if (x->main) (void)hipStreamSynchronize(x->main);
-  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots, x->d_groups, x->d_idx,
-                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines};
+  void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots,    x->d_groups, x->d_idx,
+                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines,  x->d_fpw};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   x->h_slots.release();
@@ -582,6 +585,7 @@ static void exec_destroy(Exec* x) {
   x->h_ss.release();
   x->h_ps.release();
   x->h_verdict.release();
+  x->h_fpw.release();
   if (x->d_gu1) (void)hipFree(x->d_gu1);
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
@@ -754,8 +758,13 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   return BGV_OK;
 }
 
-// After pass 1: statuses, verdicts and the retry units of one call.
-static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, const int32_t* verdict) {
+static bool pattern_eligible(const Call* call, size_t u);
+
+// After pass 1: statuses, verdicts and the retry units of one call.  fpw_w (nullable): per
+// group of the call, the weight w the first pass's weighted test identified (run_pass1; slot
+// w - 1 is the group's one invalid slot), 0 where there was no test or no single match.
+static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, const int32_t* verdict,
+                             const uint8_t* fpw_w) {
   Layout& L = call->L;
   const uint32_t nslots = (uint32_t)L.slots.size(), ngroups = (uint32_t)L.groups.size();
   for (uint32_t i = 0; i < nslots; ++i)
@@ -816,6 +825,42 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
     }
   }
   for (char r : group_retried) call->st.batch_retries += r;
+  if (!fpw_w) return;
+  // A unit whose group's weighted test found one invalid slot is decided now: with exactly one
+  // invalid slot k the test's value is the group's raised to k + 1 (and to no other w <= 64), so
+  // the job holding slot k is invalid and every other job of the unit -- all of whose slots lie
+  // in the group and are valid -- passes, as the reference's per-set retry would find
+  // (worker.ts:76-98).  The others (two or more invalid jobs) keep their unit for the retry rounds.
+  size_t keep = 0;
+  for (size_t u = 0; u < call->units.size(); ++u) {
+    const int ug = call->unit_group[u];
+    const uint32_t w = ug >= 0 ? fpw_w[ug] : 0;
+    size_t bad = SIZE_MAX;
+    if (w && pattern_eligible(call, u)) {
+      const uint32_t k = L.groups[ug].first_slot + (w - 1);
+      for (size_t j : call->units[u]) {
+        const uint32_t f0 = L.job_first_slot[j];
+        if (k >= f0 && k < f0 + call->jobs[j].n_sets) bad = j;
+      }
+    }
+    if (bad != SIZE_MAX) {
+      for (size_t j : call->units[u]) call->code[j] = j == bad ? 0 : 1;
+      continue;
+    }
+    if (keep != u) {
+      call->units[keep] = std::move(call->units[u]);
+      call->unit_group[keep] = call->unit_group[u];
+      call->unit_rounds[keep] = call->unit_rounds[u];
+      call->unit_idx[keep] = std::move(call->unit_idx[u]);
+      call->unit_dmask[keep] = call->unit_dmask[u];
+    }
+    ++keep;
+  }
+  call->units.resize(keep);
+  call->unit_group.resize(keep);
+  call->unit_rounds.resize(keep);
+  call->unit_idx.resize(keep);
+  call->unit_dmask.resize(keep);
 }
 
 // A unit from pass 1 is pattern-testable when its jobs lie only in its group and cover every
@@ -863,39 +908,15 @@ static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int
 
 // Group testing for one retry round: split every pending unit into parts.  gb: the call's
 // first group in the batch when the first pass's u values are on the device (pattern tests
-// possible), else -1.  weighted: the round's closing supports weighted tests (k_final12).
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb, bool weighted) {
+// possible), else -1.
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb) {
   call->parts.clear();
   call->punits.clear();
   for (size_t ui = 0; ui < call->units.size(); ++ui) {
     const auto& u = call->units[ui];
     const int ug = call->unit_group[ui], urounds = call->unit_rounds[ui];
     const bool in_group = unit_in_group(call, u, ug);
-    const bool eligible = gb >= 0 && in_group && (urounds == 0 || urounds == -1) && u.size() >= 2 &&
-                          pattern_eligible(call, ui);
-    bool single_sets = true;
-    for (size_t j : u) single_sets = single_sets && call->jobs[j].n_sets == 1;
-    if (eligible && weighted && urounds == 0 && single_sets) {
-      PatternUnit pu;
-      pu.group = (uint32_t)ug;
-      pu.kind = 2;
-      const bgv_dgroup& g = call->L.groups[pu.group];
-      uint64_t m = 0;
-      for (size_t j : u) {
-        pu.jobs.push_back(j);
-        m |= job_mask(call, j, g);
-      }
-      Part part;
-      part.jobs = u;
-      part.groups.push_back((uint32_t)rg.size());
-      part.pattern = (int)call->punits.size();
-      pu.tests.push_back((uint32_t)rg.size());
-      rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1),
-                              BGV_GROUP_WEIGHTED});
-      call->parts.push_back(std::move(part));
-      call->punits.push_back(std::move(pu));
-      continue;
-    }
+    const bool eligible = gb >= 0 && in_group && urounds == 0 && u.size() >= 2 && pattern_eligible(call, ui);
     if (eligible) {
       PatternUnit pu;
       pu.group = (uint32_t)ug;
@@ -1025,27 +1046,6 @@ static void call_after_round(Call* call, const int32_t* rv) {
     }
   }
   for (const PatternUnit& pu : call->punits) {
-    if (pu.kind == 2) {  // weighted test (see PatternUnit): the identified job, or pattern tests next
-      const int32_t v = rv[pu.tests[0]];
-      const uint32_t w = ((uint32_t)v >> 8) & 0xff;
-      const bgv_dgroup& g = call->L.groups[pu.group];
-      size_t bad = SIZE_MAX;
-      if (!(v & 1) && w >= 1)
-        for (size_t j : pu.jobs)
-          if (call->L.job_first_slot[j] == g.first_slot + (w - 1)) bad = j;
-      if (trace_on()) fprintf(stderr, "[bgv]   weighted unit: %zu jobs, w %u%s\n", pu.jobs.size(), w,
-                              bad == SIZE_MAX ? " (pattern tests next)" : "");
-      if (bad != SIZE_MAX) {
-        for (size_t j : pu.jobs) call->code[j] = j == bad ? 0 : 1;
-      } else {
-        call->units.push_back(pu.jobs);
-        call->unit_group.push_back((int)pu.group);
-        call->unit_rounds.push_back(-1);
-        call->unit_idx.emplace_back();
-        call->unit_dmask.push_back(0);
-      }
-      continue;
-    }
     if (pu.kind == 1) {  // pairs and single jobs (see PatternUnit)
       std::vector<size_t> failing;
       for (size_t t = 0; t < pu.tests.size(); ++t)
@@ -1129,6 +1129,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   // merge the calls' layouts
   uint32_t nslots = 0, ngroups = 0;
   size_t nidx = 0, npkb = 0, nuniq = 0;
+  bool any_shared = false;
   for (Call* call : calls) {
     call->slot_base = nslots;
     nslots += (uint32_t)call->L.slots.size();
@@ -1136,10 +1137,15 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     nidx += call->L.idx.size();
     npkb += call->L.pkb.size();
     nuniq += call->L.uniq.size();
+    for (char sh : call->L.group_shared) any_shared = any_shared || sh;
   }
+  // the failing shared groups' weighted tests right after the closing (bgv_launch_fpw_*): bulk
+  // batches (k_final12 closes them); their groups, pairs and verdicts use a second ngroups-entry
+  // region of the group arrays
+  const bool fpw = fpw_enabled() && any_shared && nslots + ngroups > bgv_fold_pairs_max();
   HIPCHK(hipSetDevice(d.id));
   int rc;
-  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
+  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, fpw ? 2 * ngroups : ngroups)) ||
       (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx + nuniq, 1))) ||
       (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
     return rc;
@@ -1149,7 +1155,11 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   HIPCHK(x.h_pkb.reserve(npkb));
   HIPCHK(x.h_ss.reserve(nslots));
   HIPCHK(x.h_ps.reserve(nslots));
-  HIPCHK(x.h_verdict.reserve(std::max<size_t>(ngroups, 1)));
+  HIPCHK(x.h_verdict.reserve(std::max<size_t>(fpw ? 2 * ngroups : ngroups, 1)));
+  if (fpw) {
+    if ((rc = grow(&x.d_fpw, &x.fpw_cap, 1 + (size_t)ngroups))) return rc;
+    HIPCHK(x.h_fpw.reserve(1 + (size_t)ngroups));
+  }
   bgv_dslot* slots = x.h_slots.p;
   bgv_dgroup* groups = x.h_groups.p;
   uint32_t max_npk = 0;
@@ -1165,7 +1175,11 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
         max_npk = std::max(max_npk, s.n_pk);
         slots[ns++] = s;
       }
-      for (bgv_dgroup g : call->L.groups) groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots, g.mask};
+      for (size_t gi = 0; gi < call->L.groups.size(); ++gi) {
+        const bgv_dgroup& g = call->L.groups[gi];
+        groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots, g.mask, 0,
+                                  call->L.group_shared[gi] ? BGV_GROUP_SHARED : 0u};
+      }
       if (!call->L.idx.empty()) memcpy(x.h_idx.p + ni, call->L.idx.data(), 4 * call->L.idx.size());
       ni += call->L.idx.size();
       if (!call->L.pkb.empty()) memcpy(x.h_pkb.p + npb, call->L.pkb.data(), call->L.pkb.size());
@@ -1215,11 +1229,30 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   }
   const auto tg = std::chrono::steady_clock::now();
   HIPCHK(bgv_launch_groups(b, S, false));
+  if (fpw) {
+    bgv_dgroup* tgr = x.d_groups + ngroups;
+    HIPCHK(bgv_launch_fpw_list(b, tgr, x.d_fpw + 1, x.d_fpw, x.main));
+    HIPCHK(bgv_launch_fpw_pairs(b, tgr, x.d_fpw, x.main));
+    HIPCHK(bgv_launch_fpw_close(b, tgr, x.d_fpw, x.main));
+    HIPCHK(hipMemcpyAsync(x.h_fpw.p, x.d_fpw, 4ull * (1 + ngroups), hipMemcpyDeviceToHost, x.main));
+  }
   HIPCHK(hipEventRecord(x.ev1, x.main));
   HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
   HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
-  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.main));
+  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * (fpw ? 2 * ngroups : ngroups), hipMemcpyDeviceToHost, x.main));
   HIPCHK(hipStreamSynchronize(x.main));
+  // the weighted tests' identifications per first-pass group (0: none)
+  std::vector<uint8_t> fpw_w;
+  uint32_t nfpw = 0;
+  if (fpw) {
+    fpw_w.assign(ngroups, 0);
+    nfpw = std::min<uint32_t>(x.h_fpw.p[0], ngroups);
+    for (uint32_t i = 0; i < nfpw; ++i) {
+      const uint32_t g = x.h_fpw.p[1 + i];
+      const int32_t v = verdict[ngroups + i];
+      if (g < ngroups && !(v & 1)) fpw_w[g] = (uint8_t)(((uint32_t)v >> 8) & 0xff);
+    }
+  }
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
   if (prof) prof_add(c, x, true, true);
@@ -1231,7 +1264,13 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     uint32_t gb = 0;
     for (Call* call : calls) {
       call->st.device_ms += ms;
-      call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb);
+      if (fpw)
+        for (uint32_t i = 0; i < nfpw; ++i) {
+          const uint32_t g = x.h_fpw.p[1 + i];
+          if (g >= gb && g < gb + call->L.groups.size()) call->st.device_groups++;
+        }
+      call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb,
+                       fpw ? fpw_w.data() + gb : nullptr);
       call_gb.push_back(gb);
       gb += (uint32_t)call->L.groups.size();
       for (size_t u = 0; u < call->units.size() && !want_gu; ++u) want_gu = pattern_eligible(call, u);
@@ -1297,8 +1336,6 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
   int rc;
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
-  // weighted tests need k_final12's closing: rounds over more slots than the latency path takes
-  const bool weighted = c->weighted && nslots > bgv_fold_pairs_max();
   // retry rounds over the per-slot results on the device
   for (;;) {
     const auto th = std::chrono::steady_clock::now();
@@ -1306,7 +1343,7 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     std::vector<uint32_t> base;
     for (size_t k = 0; k < calls.size(); ++k) {
       base.push_back((uint32_t)rg.size());
-      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1, weighted);
+      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1);
     }
     if (rg.empty()) break;
     ++rounds;
@@ -1527,8 +1564,6 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
   {
     const char* fi = getenv("BGV_FAULT_INJECT");
     c->fault_inject = fi && atoi(fi) > 0;
-    const char* we = getenv("BGV_WEIGHTED");
-    c->weighted = we && atoi(we) > 0;
   }
   c->max_slots = (uint32_t)max_batch_slots();
   c->coalesce = (uint32_t)coalesce_us();

@@ -92,6 +92,14 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
 // nslots + ngroups exceeds this (else k_final_fold)
 uint32_t bgv_fold_pairs_max();
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
+// The first pass's weighted tests of its failing groups (bulk batches, after bgv_launch_groups
+// on the same stream; bgv_k_final.hip): list (tg / list / *dcount, at most b.ngroups), pairs,
+// closing.  tg and the tests' sums, pairs and verdicts are the entries [b.ngroups, 2 b.ngroups)
+// of the group arrays (the Exec reserves twice the groups).
+hipError_t bgv_launch_fpw_list(const bgv_dev_batch& b, bgv_dgroup* tg, uint32_t* list, uint32_t* dcount,
+                               hipStream_t st);
+hipError_t bgv_launch_fpw_pairs(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st);
+hipError_t bgv_launch_fpw_close(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st);
 size_t bgv_slot_bytes();
 size_t bgv_slot_mem_bytes(uint32_t cap_slots);  // the per-slot arrays of an Exec of cap_slots slots
 size_t bgv_group_bytes();

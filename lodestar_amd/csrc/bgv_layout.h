@@ -55,3 +55,6 @@ struct bgv_dgroup {
 };
 #define BGV_ALL_SLOTS (~0ull)
 #define BGV_GROUP_WEIGHTED 1u
+// a first-pass group shared by several batchable jobs (only such a group is retried per job,
+// so only its failure takes the first pass's weighted test, bgv_launch_fpw_list)
+#define BGV_GROUP_SHARED 2u

@@ -192,20 +192,12 @@ def test_split_epoch_sweep_2p20(split_ctxs):
 # ---------------------------------------------------------------------------------------
 @pytest.fixture(scope="module")
 def weighted_ctx():
-    """A context with the weighted retry tests on (BGV_WEIGHTED=1 is read at bgv_init)."""
-    import os
+    """A context with 20,480 cached keys.  Round 5: the weighted tests run in the first pass of
+    every bulk batch (bgv_launch_fpw_*, on by default; BGV_FPW=0 turns them off)."""
     from lodestar_amd import native
     n = 20480
     sks = [_interop_sk(i) for i in range(n)]
-    old = os.environ.get("BGV_WEIGHTED")
-    os.environ["BGV_WEIGHTED"] = "1"
-    try:
-        c = native.Context([0])
-    finally:
-        if old is None:
-            del os.environ["BGV_WEIGHTED"]
-        else:
-            os.environ["BGV_WEIGHTED"] = old
+    c = native.Context([0])
     c.keygen(b"".join(sks), cache_first=0, want_pubkeys=False)
     yield c, sks
     c.close()
@@ -235,7 +227,7 @@ def test_weighted_retry_large_call(weighted_ctx):
     st = native.BgvStats()
     got = c.verify_jobs([([s], True) for s in sets], native.MODE_WORKER, stats=st)
     assert got == want
-    # 320 first-pass groups, 8 failing: one weighted test each; the six single-invalid groups
-    # are resolved there, the two- and three-invalid groups take 2 x 6 pattern tests and then
-    # pairs / single jobs.  Without identifications it would be >= 320 + 8 + 8 x 6.
+    # 320 first-pass groups, 8 failing: one weighted test each in the first pass; the six
+    # single-invalid groups are resolved there, the two- and three-invalid groups take 2 x 6
+    # pattern tests and then pairs / single jobs.  Without identifications it would be >= 320 + 8 x 6.
     assert st.device_groups < 320 + 8 + 8 * 6, st.device_groups

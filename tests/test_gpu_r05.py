@@ -87,3 +87,33 @@ def test_split_min_one_acts_as_two(ctxs):
         assert two.verify_jobs([([wrong], False)], native.MODE_WORKER) == [0]
     finally:
         two.set_split(2048)
+
+
+# ---------------------------------------------------------------------------------------
+# The first pass's weighted tests (bgv_launch_fpw_*, bgv_api.cpp call_after_pass1): every failing
+# shared group of a bulk batch takes one weighted test right after the closing; a group with one
+# invalid slot is decided from the first pass.  Multi-set batchable jobs: a job inside one group
+# is identified by its slot; jobs that straddle two groups are not pattern-eligible and keep the
+# retry rounds.  Every verdict must equal the job verified alone (BGV_MODE_PER_JOB;
+# chain/bls/multithread/worker.ts:76-98).
+# ---------------------------------------------------------------------------------------
+def test_first_pass_weighted_tests_multi_set_jobs(ctxs):
+    from lodestar_amd import native
+    (one, _), sks = ctxs
+    n = 6000 * 3  # 18,000 sets > BGV_LATENCY_MAX: a bulk batch
+    roots = [hashlib.sha256(b"r05-fpw-%d" % (i // 7)).digest() for i in range(n)]
+    keys = [i % NKEYS for i in range(n)]
+    sigs = one.sign(b"".join(sks[k] for k in keys), b"".join(roots))
+    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[keys[i]]) for i in range(n)]
+    # wrong messages: one per group at various slots, two in one job, one in a job that straddles
+    # groups 20 / 21 (slots 1278..1280 hold sets 1278, 1279 | 1280), three in one group
+    for i in (5, 64 * 4 + 63, 64 * 7 + 30, 64 * 9 + 1, 64 * 9 + 2, 1279, 64 * 40 + 3, 64 * 40 + 20,
+              64 * 40 + 41, n - 1):
+        sets[i] = native.SetSpec(roots[(i + 700) % n], sets[i].sig, pk_indices=list(sets[i].pk_indices))
+    jobs = [(sets[3 * j:3 * j + 3], True) for j in range(n // 3)]
+    st = native.BgvStats()
+    got = one.verify_jobs(jobs, native.MODE_WORKER, stats=st)
+    want = one.verify_jobs(jobs, native.MODE_PER_JOB)
+    assert got == want
+    assert sum(1 for v in got if v != 1) == 9  # ten wrong sets, two of them in one job
+    assert st.batch_retries >= 6
