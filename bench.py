@@ -158,10 +158,23 @@ def default_batching():
     return env("BGV_MAX_BATCH_SLOTS", 131072), env("BGV_COALESCE_US", 500), env("BGV_IDLE_COALESCE_US", 50)
 
 
+def undecodable_signatures():
+    """Two committed signature encodings that fail to decode beyond a flag bit: an x with no
+    curve point (BLST_POINT_NOT_ON_CURVE) and a curve point outside G2 (BLST_POINT_NOT_IN_GROUP),
+    the `off_curve` / `not_in_g2` jobs of tests/golden/verdicts.json (data, generated by
+    tools/gen_golden.py with the oracle)."""
+    jobs = json.load(open(os.path.join(ROOT, "tests", "golden", "verdicts.json")))["jobs"]
+    by = {j["name"]: j for j in jobs}
+    return (bytes.fromhex(by["off_curve"]["sets"][0]["sig"]), -2), (bytes.fromhex(by["not_in_g2"]["sets"][0]["sig"]), -3)
+
+
 def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0x8192, committee=1):
     """config 4: nsets single sets over distinct validators, distinct signing roots,
-    1 % corrupted at random.Random(0x8192).sample positions, three classes.  committee > 1:
-    mainnet-shaped roots, one per `committee` consecutive sets (SURVEY 8(d) "Messages")."""
+    1 % corrupted at random.Random(0x8192).sample positions: a third wrong messages, a third
+    wrong keys (false), a third undecodable -- cycling through a flipped compression flag
+    (BLST_BAD_ENCODING), an x off the curve (BLST_POINT_NOT_ON_CURVE) and a point outside G2
+    (BLST_POINT_NOT_IN_GROUP), SURVEY 8(d) config 4.  committee > 1: mainnet-shaped roots, one per
+    `committee` consecutive sets (SURVEY 8(d) "Messages")."""
     key_of = [(rank * nsets + i * 7919) % nkeys for i in range(nsets)]
     msgs = [hashlib.sha256(b"lodestar-bench" + rank.to_bytes(4, "little") + (i // committee).to_bytes(4, "little"))
             .digest() for i in range(nsets)]
@@ -169,6 +182,7 @@ def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0
     sigs = [sigs_raw[96 * i:96 * i + 96] for i in range(nsets)]
     expect = [1] * nsets
     bad = random.Random(seed).sample(range(nsets), int(round(nsets * corrupt_frac)))
+    undecodable = undecodable_signatures()
     for j, i in enumerate(bad):
         if j % 3 == 0:
             msgs[i] = hashlib.sha256(b"wrong" + msgs[i]).digest()
@@ -176,9 +190,11 @@ def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0
         elif j % 3 == 1:
             key_of[i] = (key_of[i] + 1) % nkeys
             expect[i] = 0
-        else:
+        elif (j // 3) % 3 == 0:
             sigs[i] = bytes([sigs[i][0] & 0x7F]) + sigs[i][1:]
             expect[i] = -1
+        else:
+            sigs[i], expect[i] = undecodable[(j // 3) % 3 - 1]
     jobs = [([native.SetSpec(msgs[i], sigs[i], pk_indices=[key_of[i]])], True) for i in range(nsets)]
     return jobs, expect, key_of
 
@@ -601,6 +617,80 @@ def epoch_sweep(ctx, native, barrier, rank, world, nsets=EPOCH_SETS, committee=E
             "ms": 1e3 * elapsed, "setup_s": setup_s, "verdicts": {"valid": code, "two_swapped_signatures": bad}}
 
 
+def node_shape(native, devices, nkeys, steps, warmup, settle_s, sweep=True):
+    """The beacon node's own multi-GPU shape: ONE process drives every
+    device through one context, Context(devices), and libblsgpu spreads each big call over them
+    (bgv_set_split; the reference's split of a big call over its workers,
+    chain/bls/multithread/index.ts:153-166).  Two workloads, beside the rank-based headline:
+      gossip  config 4 mode (ii): the same stream of 8192-set calls (8192 batchable one-set jobs,
+              1 % corrupted) as the headline, each call cut into one run of jobs per device;
+              sets/s over whole completion periods after warmup and the settle time
+      sweep   config 5 as one call: 2^20 single sets in ONE job, cut into one run per device whose
+              Fp12 Miller-loop partials meet in one final exponentiation; valid, then with two
+              signatures swapped (false)
+    Every verdict is checked.  devices may repeat an index: Context([0, 0]) rehearses the
+    two-device split on one GPU (tests/test_gpu_r04.py checks its verdicts against Context([0]))."""
+    ctx = native.Context(list(devices))
+    try:
+        t0 = time.perf_counter()
+        nk = max(nkeys, EPOCH_SETS if sweep else nkeys)
+        sks = [interop_sk(i) for i in range(nk)]
+        for lo in range(0, nk, 1 << 17):
+            ctx.keygen(b"".join(sks[lo:lo + (1 << 17)]), cache_first=lo, want_pubkeys=False)
+        jobs, expect, _ = make_gossip_batch(ctx, native, 0, 8192, nkeys)
+        packed = native.PackedCall(jobs)
+        setup_s = time.perf_counter() - t0
+
+        def step():
+            out = (native.ctypes.c_int32 * len(jobs))()
+            st = native.BgvStats()
+            rc = ctx.lib.bgv_verify(ctx.handle, packed.jobs, len(jobs), packed.sets, packed.nsets,
+                                    native.MODE_WORKER, out, native.ctypes.byref(st))
+            if rc != 0:
+                raise native.DeviceError(native.strerror(rc))
+            return list(out), st
+
+        nd = len(devices)
+        # a split call becomes nd pinned shard calls of 8192 / nd sets; each device's dispatchers
+        # merge the shards in flight into super-batches of the library's default geometry, so
+        # completions repeat every (calls per device super-batch) x dispatchers calls
+        per_batch = super_batch_calls(max(1, 8192 // nd))
+        ncalls = timed_calls(steps, per_batch, int(os.environ.get("BGV_DISPATCHERS", "2")))
+        win = stream_window(step, expect, warmup, ncalls, max(32, 3 * per_batch), settle_s=settle_s,
+                            boundary=per_batch)
+        out = {"devices": list(devices), "setup_s": setup_s,
+               "gossip": {"value": 8192 * ncalls / win["elapsed"], "unit": "sets/s", "calls_timed": ncalls,
+                          "p50_call_latency_ms": 1e3 * statistics.median(win["latencies"]),
+                          "config": "config4 mode (ii): 8192-set calls (8192 batchable one-set jobs, 1%% corrupted) "
+                                    "each cut into %d device runs by bgv_set_split, one process" % nd}}
+        if sweep:
+            n = EPOCH_SETS
+            roots = [hashlib.sha256(b"lodestar-epoch" + c.to_bytes(4, "little")).digest()
+                     for c in range(n // EPOCH_COMMITTEE)]
+            msgs = b"".join(roots[i // EPOCH_COMMITTEE] for i in range(n))
+            sigs = bytearray()
+            for lo in range(0, n, 1 << 17):
+                sigs += ctx.sign(b"".join(sks[lo:lo + (1 << 17)]), msgs[32 * lo:32 * (lo + (1 << 17))])
+            one = native.PackedSingleSets(msgs, bytes(sigs), range(n))
+            assert ctx.verify_packed_one_job(one) == 1, "node-shape sweep: valid sweep rejected"  # warm
+            cuda_sync()
+            t1 = time.perf_counter()
+            code = ctx.verify_packed_one_job(one)
+            dt = time.perf_counter() - t1
+            assert code == 1, "node-shape sweep verdict %r" % code
+            a, b = 1000, n - 1000
+            sigs[96 * a:96 * a + 96], sigs[96 * b:96 * b + 96] = sigs[96 * b:96 * b + 96], sigs[96 * a:96 * a + 96]
+            bad = ctx.verify_packed_one_job(native.PackedSingleSets(msgs, bytes(sigs), range(n)))
+            assert bad == 0, "node-shape sweep: swapped signatures verdict %r" % bad
+            out["sweep"] = {"value": n / dt, "unit": "sets/s", "ms": 1e3 * dt, "sets": n,
+                            "verdicts": {"valid": code, "two_swapped_signatures": bad},
+                            "config": "config5 as ONE job of 2^20 single sets, cut into %d device runs (Fp12 "
+                                      "partials, one final exponentiation), one process" % nd}
+        return out
+    finally:
+        ctx.close()
+
+
 # PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
 TRAFFIC_FILE = os.path.join("profiles", "r04", "traffic.json")
 ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
@@ -652,6 +742,9 @@ def main():
                     help="calls merged per device super-batch (default: the library's default geometry, "
                          "BGV_MAX_BATCH_SLOTS // --nsets = 16 calls of 8192 sets)")
     ap.add_argument("--no-epoch-sweep", action="store_true", help="skip the config-5 sweep leg")
+    ap.add_argument("--node-shape", choices=["auto", "on", "off"], default="auto",
+                    help="the single-process leg over Context(range(N)) with bgv_set_split (rank 0, after the "
+                         "timed region): auto = at N > 1 only; at N = 1 'on' rehearses it on Context([0, 0])")
     ap.add_argument("--check-ranks", action="store_true",
                     help="preflight: start the ranks, join the process group, print one line naming the ranks "
                          "and the backend, exit (no GPU work)")
@@ -734,6 +827,13 @@ def main():
         agg = aggregate_throughput(ctx, native, args.nkeys, settle_s=args.settle_s)
         mainnet = mainnet_shaped_throughput(ctx, native, args.nkeys, settle_s=args.settle_s)
     sweep = None if args.no_epoch_sweep else epoch_sweep(ctx, native, barrier, rank, world)
+    shape = None
+    if args.node_shape == "on" or (args.node_shape == "auto" and world > 1):
+        # rank 0 alone, while the other ranks wait at the barrier with their devices idle
+        if rank == 0:
+            devs = list(range(world)) if world > 1 else [local, local]
+            shape = node_shape(native, devs, args.nkeys, 64, 16, args.settle_s, sweep=not args.no_epoch_sweep)
+        barrier()
 
     if rank == 0:
         total_sets = args.nsets * ncalls * world
@@ -785,7 +885,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u32 (28-bit-limb Montgomery Fp, v_mad_u64_u32)",
             "data": "synthetic: interop validator keys (%d in the device cache), distinct 32-B signing roots, "
-                    "device-signed; 1%% corrupted (wrong msg / wrong key / bad encoding)" % args.nkeys,
+                    "device-signed; 1%% corrupted (wrong msg / wrong key / undecodable: bad encoding, off curve, "
+                    "not in G2)" % args.nkeys,
             "config": {"workload": "config4: 8192-set gossip batch (8192 batchable one-set jobs, BGV_MODE_WORKER, "
                                    "batch-fail -> per-job retry)", "sets_per_batch": args.nsets,
                        "batches_in_flight": max(args.inflight, 3 * bcalls), "calls_per_super_batch": bcalls,
@@ -825,6 +926,8 @@ def main():
             line["mainnet_shaped_roots"] = mainnet
         if sweep is not None:
             line["epoch_sweep"] = sweep
+        if shape is not None:
+            line["node_single_process"] = shape
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cb = cpu_baseline(jobs, key_of, expect, min(args.nsets, args.cpu_sample), args.cpu_seconds)
             line["cpu_baseline"] = cb
