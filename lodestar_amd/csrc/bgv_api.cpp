@@ -112,15 +112,19 @@ static int execs_per_device() {
 // Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
 // retry rounds of several super-batches then run side by side instead of queueing behind one
 // another (their rounds are latency-bound chains of small launches)
-// BGV_FPW=0 turns off the first pass's weighted tests of its failing groups (run_pass1), for
-// A/B measurements; on by default
-static bool fpw_enabled() {
+// BGV_UNIFORM=0 turns off uniform groups (BGV_GROUP_UNIFORM: one Miller loop per group whose sets
+// share a signing root, and the grouping of a call's batchable one-set jobs by root that makes
+// them), for A/B measurements; on by default
+static bool uniform_enabled() {
   static const bool v = [] {
-    const char* e = getenv("BGV_FPW");
+    const char* e = getenv("BGV_UNIFORM");
     return !(e && atoi(e) == 0);
   }();
   return v;
 }
+// calls with fewer batchable one-set jobs take the latency path: their jobs keep their order
+#define BGV_UNIFORM_MIN_JOBS 1024
+
 static int retry_threads_per_device() {
   static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
   return v;
@@ -191,11 +195,10 @@ struct Exec {
   size_t pout_cap = 0;
   uint32_t* d_lines = nullptr;  // the bulk Miller loop's line records (bgv_lines_pairs)
   uint32_t lines_cap = 0;       // pairs
-  // the first pass's weighted tests (bgv_launch_fpw_*): [0] their count, [1 + i] test i's
-  // first-pass group; host mirror
-  uint32_t* d_fpw = nullptr;
-  size_t fpw_cap = 0;
-  Pinned<uint32_t> h_fpw;
+  // the failing uniform first-pass groups whose slots' own pairs the retry thread computes
+  // (bgv_launch_uniform_refill): [0] their count, [1 + i] group i
+  uint32_t* d_ulist = nullptr;
+  size_t ulist_cap = 0;
 };
 
 // bgv_final_verify's device buffers (under util_mu)
@@ -217,6 +220,7 @@ struct BatchState {
   uint32_t nslots = 0, ngroups = 0;
   std::vector<uint32_t> call_gb;  // each call's first group in the merged batch
   bool want_gu = false;           // the first pass's u values are in x.d_gu1 (pattern tests)
+  std::vector<uint32_t> refill;   // failing uniform groups of shared jobs: their slots' own pairs first
   bool prof = false;
 };
 // A super-batch whose first pass is done and whose retry rounds wait for the retry thread.
@@ -263,6 +267,8 @@ struct Layout {
   std::vector<std::vector<uint32_t>> job_groups;
   std::vector<uint32_t> job_first_slot;  // first slot of each laid-out job (its slots are contiguous)
   std::vector<char> group_shared;        // group holds sets of more than one job
+  std::vector<char> group_uniform;       // every set of the group shares one signing root and every
+                                         // job in it lies inside it (BGV_GROUP_UNIFORM in bulk batches)
   std::vector<uint32_t> idx;             // concatenated pubkey indices
   std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
   std::vector<uint32_t> uniq;            // first slot of each distinct signing root (hash_to_G2 once)
@@ -287,6 +293,7 @@ struct Builder {
     while (L.slots.size() < aligned) pad();
     L.groups.push_back(bgv_dgroup{aligned, 0, BGV_ALL_SLOTS});
     L.group_shared.push_back(0);
+    L.group_uniform.push_back(1);
     open_group = (uint32_t)L.groups.size() - 1;
     open = true;
     open_job = -1;
@@ -336,6 +343,7 @@ struct Builder {
       s.hsrc = self;
       L.uniq.push_back(self);
     }
+    if (g.n_slots > 0 && L.slots[g.first_slot].hsrc != s.hsrc) L.group_uniform[open_group] = 0;
     L.slots.push_back(s);
     L.slot_set.push_back((int32_t)set_index);
     g.n_slots++;
@@ -371,10 +379,6 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // both its jobs are invalid (for b in D, S_b and its complement each hold an invalid job, and
 // every invalid job is a candidate of that one pair); a failing single job is invalid; jobs of
 // a failing pair next to other failures are tested alone in one more round.
-//
-// A failing shared group of a bulk batch has already had ONE weighted test in the first pass
-// (run_pass1, bgv_launch_fpw_*): a group with exactly one invalid slot is decided there, so the
-// units that reach the retry rounds hold two or more invalid jobs (or were not testable).
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
   int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs
@@ -575,7 +579,7 @@ static int exec_create(Exec* x) {
 static void exec_destroy(Exec* x) {
   if (x->main) (void)hipStreamSynchronize(x->main);
   void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots,    x->d_groups, x->d_idx,
-                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines,  x->d_fpw};
+                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines,  x->d_ulist};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   x->h_slots.release();
@@ -585,7 +589,6 @@ static void exec_destroy(Exec* x) {
   x->h_ss.release();
   x->h_ps.release();
   x->h_verdict.release();
-  x->h_fpw.release();
   if (x->d_gu1) (void)hipFree(x->d_gu1);
   if (x->ev0) (void)hipEventDestroy(x->ev0);
   if (x->ev1) (void)hipEventDestroy(x->ev1);
@@ -734,12 +737,56 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
     B.close_group();
   }
   B.close_group();
-  for (size_t j : call->todo) {
-    if (!call->shared_job(j)) continue;
+  // Batchable jobs share groups in any order (verdicts map by job).  One-set jobs go grouped by
+  // signing root -- the roots in order of first appearance, each root's jobs in call order -- so
+  // that the sets of a root fill whole groups (BGV_GROUP_UNIFORM: one Miller loop for the group;
+  // gossip attestations of one committee share a root); then multi-set jobs.
+  std::vector<size_t> shared_order;
+  size_t n_one = 0;
+  for (size_t j : call->todo)
+    if (call->shared_job(j) && jobs[j].n_sets == 1) ++n_one;
+  if (uniform_enabled() && n_one >= BGV_UNIFORM_MIN_JOBS) {
+    std::unordered_map<uint64_t, uint32_t> bucket_of;
+    bucket_of.reserve(2 * n_one);
+    std::vector<std::vector<size_t>> buckets;
+    std::vector<const uint8_t*> broot;
+    bool grouped = false;  // some root recurs after another root: the order changes
+    uint32_t last = UINT32_MAX;
+    for (size_t j : call->todo) {
+      if (!call->shared_job(j) || jobs[j].n_sets != 1) continue;
+      const uint8_t* m = sets[jobs[j].first_set].msg;
+      uint64_t key;
+      memcpy(&key, m, 8);
+      auto it = bucket_of.find(key);
+      uint32_t b;
+      if (it != bucket_of.end() && memcmp(broot[it->second], m, 32) == 0) {
+        b = it->second;
+      } else {  // a new root (a key collision between different roots just opens another bucket)
+        b = (uint32_t)buckets.size();
+        buckets.emplace_back();
+        broot.push_back(m);
+        if (it == bucket_of.end()) bucket_of.emplace(key, b);
+      }
+      grouped = grouped || (b != last && !buckets[b].empty());
+      last = b;
+      buckets[b].push_back(j);
+    }
+    if (grouped) {
+      for (const auto& bk : buckets) shared_order.insert(shared_order.end(), bk.begin(), bk.end());
+      for (size_t j : call->todo)
+        if (call->shared_job(j) && jobs[j].n_sets != 1) shared_order.push_back(j);
+    }
+  }
+  if (shared_order.empty())  // call order
+    for (size_t j : call->todo)
+      if (call->shared_job(j)) shared_order.push_back(j);
+  for (size_t j : shared_order)
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
-  }
   B.pad_to_wave();
+  for (size_t j : call->todo)
+    if (L.job_groups[j].size() > 1)
+      for (uint32_t g : L.job_groups[j]) L.group_uniform[g] = 0;
   call->set_sig.assign(nsets, 0);
   call->set_pk.assign(nsets, 0);
   if (L.slots.empty()) {  // nothing for the device
@@ -758,13 +805,8 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   return BGV_OK;
 }
 
-static bool pattern_eligible(const Call* call, size_t u);
-
-// After pass 1: statuses, verdicts and the retry units of one call.  fpw_w (nullable): per
-// group of the call, the weight w the first pass's weighted test identified (run_pass1; slot
-// w - 1 is the group's one invalid slot), 0 where there was no test or no single match.
-static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, const int32_t* verdict,
-                             const uint8_t* fpw_w) {
+// After pass 1: statuses, verdicts and the retry units of one call.
+static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, const int32_t* verdict) {
   Layout& L = call->L;
   const uint32_t nslots = (uint32_t)L.slots.size(), ngroups = (uint32_t)L.groups.size();
   for (uint32_t i = 0; i < nslots; ++i)
@@ -825,42 +867,6 @@ static void call_after_pass1(Call* call, const int32_t* ss, const int32_t* ps, c
     }
   }
   for (char r : group_retried) call->st.batch_retries += r;
-  if (!fpw_w) return;
-  // A unit whose group's weighted test found one invalid slot is decided now: with exactly one
-  // invalid slot k the test's value is the group's raised to k + 1 (and to no other w <= 64), so
-  // the job holding slot k is invalid and every other job of the unit -- all of whose slots lie
-  // in the group and are valid -- passes, as the reference's per-set retry would find
-  // (worker.ts:76-98).  The others (two or more invalid jobs) keep their unit for the retry rounds.
-  size_t keep = 0;
-  for (size_t u = 0; u < call->units.size(); ++u) {
-    const int ug = call->unit_group[u];
-    const uint32_t w = ug >= 0 ? fpw_w[ug] : 0;
-    size_t bad = SIZE_MAX;
-    if (w && pattern_eligible(call, u)) {
-      const uint32_t k = L.groups[ug].first_slot + (w - 1);
-      for (size_t j : call->units[u]) {
-        const uint32_t f0 = L.job_first_slot[j];
-        if (k >= f0 && k < f0 + call->jobs[j].n_sets) bad = j;
-      }
-    }
-    if (bad != SIZE_MAX) {
-      for (size_t j : call->units[u]) call->code[j] = j == bad ? 0 : 1;
-      continue;
-    }
-    if (keep != u) {
-      call->units[keep] = std::move(call->units[u]);
-      call->unit_group[keep] = call->unit_group[u];
-      call->unit_rounds[keep] = call->unit_rounds[u];
-      call->unit_idx[keep] = std::move(call->unit_idx[u]);
-      call->unit_dmask[keep] = call->unit_dmask[u];
-    }
-    ++keep;
-  }
-  call->units.resize(keep);
-  call->unit_group.resize(keep);
-  call->unit_rounds.resize(keep);
-  call->unit_idx.resize(keep);
-  call->unit_dmask.resize(keep);
 }
 
 // A unit from pass 1 is pattern-testable when its jobs lie only in its group and cover every
@@ -1129,7 +1135,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   // merge the calls' layouts
   uint32_t nslots = 0, ngroups = 0;
   size_t nidx = 0, npkb = 0, nuniq = 0;
-  bool any_shared = false;
+  bool any_uniform = false;
   for (Call* call : calls) {
     call->slot_base = nslots;
     nslots += (uint32_t)call->L.slots.size();
@@ -1137,15 +1143,14 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     nidx += call->L.idx.size();
     npkb += call->L.pkb.size();
     nuniq += call->L.uniq.size();
-    for (char sh : call->L.group_shared) any_shared = any_shared || sh;
+    for (char u : call->L.group_uniform) any_uniform = any_uniform || u;
   }
-  // the failing shared groups' weighted tests right after the closing (bgv_launch_fpw_*): bulk
-  // batches (k_final12 closes them); their groups, pairs and verdicts use a second ngroups-entry
-  // region of the group arrays
-  const bool fpw = fpw_enabled() && any_shared && nslots + ngroups > bgv_fold_pairs_max();
+  const bool bulk = nslots + ngroups > bgv_fold_pairs_max();
+  // uniform groups (BGV_GROUP_UNIFORM): bulk batches on the two-phase Miller stage
+  const bool uniform = uniform_enabled() && any_uniform && bulk && !bgv_single_pass_miller();
   HIPCHK(hipSetDevice(d.id));
   int rc;
-  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, fpw ? 2 * ngroups : ngroups)) ||
+  if ((rc = exec_reserve_slots(x, nslots)) || (rc = exec_reserve_groups(x, ngroups)) ||
       (rc = grow(&x.d_idx, &x.idx_cap, std::max<size_t>(nidx + nuniq, 1))) ||
       (rc = grow(&x.d_pkb, &x.pkb_cap, std::max<size_t>(npkb, 1))))
     return rc;
@@ -1155,11 +1160,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   HIPCHK(x.h_pkb.reserve(npkb));
   HIPCHK(x.h_ss.reserve(nslots));
   HIPCHK(x.h_ps.reserve(nslots));
-  HIPCHK(x.h_verdict.reserve(std::max<size_t>(fpw ? 2 * ngroups : ngroups, 1)));
-  if (fpw) {
-    if ((rc = grow(&x.d_fpw, &x.fpw_cap, 1 + (size_t)ngroups))) return rc;
-    HIPCHK(x.h_fpw.reserve(1 + (size_t)ngroups));
-  }
+  HIPCHK(x.h_verdict.reserve(std::max<size_t>(ngroups, 1)));
   bgv_dslot* slots = x.h_slots.p;
   bgv_dgroup* groups = x.h_groups.p;
   uint32_t max_npk = 0;
@@ -1178,7 +1179,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
       for (size_t gi = 0; gi < call->L.groups.size(); ++gi) {
         const bgv_dgroup& g = call->L.groups[gi];
         groups[ng++] = bgv_dgroup{g.first_slot + call->slot_base, g.n_slots, g.mask, 0,
-                                  call->L.group_shared[gi] ? BGV_GROUP_SHARED : 0u};
+                                  uniform && call->L.group_uniform[gi] ? BGV_GROUP_UNIFORM : 0u};
       }
       if (!call->L.idx.empty()) memcpy(x.h_idx.p + ni, call->L.idx.data(), 4 * call->L.idx.size());
       ni += call->L.idx.size();
@@ -1206,6 +1207,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   if (npkb) HIPCHK(hipMemcpyAsync(x.d_pkb, x.h_pkb.p, npkb, hipMemcpyHostToDevice, x.main));
   bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
   b.max_npk = max_npk;
+  b.uniform = uniform;
   b.uniq = x.d_idx + nidx;
   b.nuniq = (uint32_t)nuniq;
   if (int lrc = exec_reserve_lines(x, b)) return lrc;
@@ -1229,30 +1231,11 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   }
   const auto tg = std::chrono::steady_clock::now();
   HIPCHK(bgv_launch_groups(b, S, false));
-  if (fpw) {
-    bgv_dgroup* tgr = x.d_groups + ngroups;
-    HIPCHK(bgv_launch_fpw_list(b, tgr, x.d_fpw + 1, x.d_fpw, x.main));
-    HIPCHK(bgv_launch_fpw_pairs(b, tgr, x.d_fpw, x.main));
-    HIPCHK(bgv_launch_fpw_close(b, tgr, x.d_fpw, x.main));
-    HIPCHK(hipMemcpyAsync(x.h_fpw.p, x.d_fpw, 4ull * (1 + ngroups), hipMemcpyDeviceToHost, x.main));
-  }
   HIPCHK(hipEventRecord(x.ev1, x.main));
   HIPCHK(hipMemcpyAsync(ss, b.sig_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
   HIPCHK(hipMemcpyAsync(ps, b.pk_status, 4ull * nslots, hipMemcpyDeviceToHost, x.main));
-  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * (fpw ? 2 * ngroups : ngroups), hipMemcpyDeviceToHost, x.main));
+  HIPCHK(hipMemcpyAsync(verdict, b.verdict, 4ull * ngroups, hipMemcpyDeviceToHost, x.main));
   HIPCHK(hipStreamSynchronize(x.main));
-  // the weighted tests' identifications per first-pass group (0: none)
-  std::vector<uint8_t> fpw_w;
-  uint32_t nfpw = 0;
-  if (fpw) {
-    fpw_w.assign(ngroups, 0);
-    nfpw = std::min<uint32_t>(x.h_fpw.p[0], ngroups);
-    for (uint32_t i = 0; i < nfpw; ++i) {
-      const uint32_t g = x.h_fpw.p[1 + i];
-      const int32_t v = verdict[ngroups + i];
-      if (g < ngroups && !(v & 1)) fpw_w[g] = (uint8_t)(((uint32_t)v >> 8) & 0xff);
-    }
-  }
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
   if (prof) prof_add(c, x, true, true);
@@ -1264,13 +1247,13 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     uint32_t gb = 0;
     for (Call* call : calls) {
       call->st.device_ms += ms;
-      if (fpw)
-        for (uint32_t i = 0; i < nfpw; ++i) {
-          const uint32_t g = x.h_fpw.p[1 + i];
-          if (g >= gb && g < gb + call->L.groups.size()) call->st.device_groups++;
-        }
-      call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb,
-                       fpw ? fpw_w.data() + gb : nullptr);
+      call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb);
+      // a failing uniform group of shared jobs goes to the retry tests, which multiply its
+      // slots' own pairs: the retry thread computes them first (run_retries)
+      if (uniform)
+        for (size_t gi = 0; gi < call->L.groups.size(); ++gi)
+          if (call->L.group_uniform[gi] && call->L.group_shared[gi] && !(verdict[gb + gi] & 1))
+            bs.refill.push_back(gb + (uint32_t)gi);
       call_gb.push_back(gb);
       gb += (uint32_t)call->L.groups.size();
       for (size_t u = 0; u < call->units.size() && !want_gu; ++u) want_gu = pattern_eligible(call, u);
@@ -1336,6 +1319,21 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
   int rc;
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
+  if (!bs.refill.empty()) {
+    // the failing uniform groups' slots' own pairs, over the first pass's groups, slots, line
+    // records and per-slot results (x still holds them: no round has run yet)
+    const uint32_t nr = (uint32_t)bs.refill.size();
+    std::vector<uint32_t> lst(1 + nr);
+    lst[0] = nr;
+    std::copy(bs.refill.begin(), bs.refill.end(), lst.begin() + 1);
+    if ((rc = grow(&x.d_ulist, &x.ulist_cap, lst.size()))) return rc;
+    HIPCHK(hipMemcpyAsync(x.d_ulist, lst.data(), 4 * lst.size(), hipMemcpyHostToDevice, x.close));
+    b = make_batch(d, x, nslots, bs.ngroups);
+    b.lines = x.d_lines;
+    b.lines_cap = x.lines_cap;
+    HIPCHK(bgv_launch_uniform_refill(b, x.d_ulist + 1, x.d_ulist, x.close));
+    HIPCHK(hipStreamSynchronize(x.close));  // lst leaves scope
+  }
   // retry rounds over the per-slot results on the device
   for (;;) {
     const auto th = std::chrono::steady_clock::now();

@@ -70,16 +70,14 @@ __global__ void BGV_KATTR k_final(const bgv_dgroup* __restrict__ groups, uint32_
 // k_final on teams of 12 lanes, five per wave (lanes 60..63 run a sixth, idle team on LDS
 // slots of their own so every lane reaches every barrier): a fifth fewer waves for the
 // same groups.  Same products in the same order as k_final, so the same verdicts.
-// dcount (nullable): the groups are min(ngroups, *dcount), a count only the device knows (the
-// first pass's weighted tests, bgv_launch_fpw_list); whole blocks past it exit at once.
+// gpkp (nullable; first passes with uniform groups): a BGV_GROUP_UNIFORM group multiplies its
+// one pubkey-sum pair gpkp[g] instead of its slots' own pairs.
 #define BGV_FINAL12_TEAMS 5
 __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                     const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                     int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
                                     fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
-                                    const uint32_t* __restrict__ dcount) {
-  if (dcount) ngroups = min(ngroups, *dcount);
-  if (blockIdx.x * BGV_FINAL12_TEAMS >= ngroups) return;
+                                    const fp12_t* __restrict__ gpkp) {
   __shared__ fp_t lds[BGV_FINAL12_TEAMS + 1][2 * BGV_TEAM_COMPS];
   __shared__ uint32_t lens[BGV_FINAL12_TEAMS + 1];
   const int team = threadIdx.x / BGV_TEAM_COMPS, c = threadIdx.x % BGV_TEAM_COMPS;
@@ -91,11 +89,10 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
   // present ones only (a retry test masks half of a group or a single job), the teams of the
   // wave to the longest list, multiplying by 1 past their own
   uint64_t m = live ? g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1)) : 0;
-  const bool wt = live && (g.flags & BGV_GROUP_WEIGHTED);
-  if (c == 0) lens[team] = wt ? g.n_slots : (uint32_t)__popcll(m);
-  // a wave holding a weighted test runs every team through the weighted loop's shape (two
-  // products per step, the identification below), the others' extra products by 1
-  const bool anyw = __syncthreads_or(wt ? 1 : 0) != 0;
+  const bool uni = gpkp && live && (g.flags & BGV_GROUP_UNIFORM);
+  if (uni) m = 0;  // its slots' pairs are the one pair gpkp[gi]
+  if (c == 0) lens[team] = (uint32_t)__popcll(m);
+  __syncthreads();
   uint32_t nmax = 0;
   BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
   const int fi = tm_fp_index(c);
@@ -110,99 +107,18 @@ __global__ void BGV_KATTR k_final12(const bgv_dgroup* __restrict__ groups, uint3
     m &= m - 1;
     return fs[kFp12 * k + fi];
   };
-  if (!anyw) {
-    fp_t y = next();
-    BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
-      const fp_t yn = next();  // next operand in flight
-      x = o.mul(x, y);
-      y = yn;
-    }
-  } else {
-    // weighted teams: positions k = n_slots - 1 .. 0, S = prod_{k' >= k} f_k' (1 where absent),
-    // x = gpair * prod_k S_k = gpair * prod_k f_k^(k+1); the others: x = x * (next present)
-    const uint64_t mw = m;
-    uint32_t kk = wt ? g.n_slots : 0;
-    fp_t S = one_c;
-    BGV_NO_UNROLL for (uint32_t step = 0; step < nmax; ++step) {
-      fp_t y;
-      const bool more = kk > 0;  // a weighted team past its last position multiplies by 1
-      if (wt) {
-        y = one_c;
-        if (more) {
-          --kk;
-          if ((mw >> kk) & 1) y = fs[kFp12 * kk + fi];
-        }
-      } else {
-        y = next();
-      }
-      const fp_t r1 = o.mul(wt ? S : x, y);
-      const fp_t r2 = o.mul(wt ? x : one_c, wt && more ? r1 : one_c);
-      if (wt) {
-        S = r1;
-        x = r2;
-      } else {
-        x = r1;
-      }
-    }
+  fp_t y = next();
+  BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
+    const fp_t yn = next();  // next operand in flight
+    x = o.mul(x, y);
+    y = yn;
   }
+  if (gpkp) x = o.mul(x, uni ? reinterpret_cast<const fp_t*>(gpkp + gi)[fi] : one_c);  // grid-uniform branch
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  int32_t v = verdict_bits(o, u, g, gu1, fi);
-  if (anyw && gu1) {
-    // identification: the first w with (value of ref1 - 1)^w == this value, i.e. u_ref^w conj(u)
-    // in Fp6 (values conj(u) / u); P = u_ref^w
-    const fp_t ur = wt && g.ref1 ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : one_c;
-    const fp_t cu = o.conj(u);
-    fp_t P = ur;
-    int32_t found = 0;
-    BGV_NO_UNROLL for (uint32_t w = 1; w <= nmax; ++w) {
-      const bool hit = o.is_fp6(o.mul(P, cu));
-      if (wt && g.ref1 && hit && found == 0 && w <= g.n_slots) found = (int32_t)w;
-      P = o.mul(P, ur);
-    }
-    if (wt) v = (v & 1) | (found << 8);
-  }
+  const int32_t v = verdict_bits(o, u, g, gu1, fi);
   if (live && c == 0) verdict[gi] = v;
-}
-
-// The first pass's weighted tests (see bgv_launch_fpw_list): one block of 256 threads lists
-// the failing groups of the first pass's closing (verdict bit 0 clear, at least two slots,
-// shared by several batchable jobs: BGV_GROUP_SHARED) in
-// group order as weighted test groups tg[i] = (the group's slots, weight k + 1 for slot k,
-// ref1 = g + 1), first-pass group index list[i], and their count.
-#define BGV_FPW_THREADS 256
-__global__ void __launch_bounds__(BGV_FPW_THREADS) k_fpw_list(const int32_t* __restrict__ verdict, uint32_t ngroups,
-                                                             const bgv_dgroup* __restrict__ groups,
-                                                             bgv_dgroup* __restrict__ tg, uint32_t* __restrict__ list,
-                                                             uint32_t* __restrict__ count) {
-  __shared__ uint32_t wave_n[BGV_FPW_THREADS / 64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t base = 0;
-  for (uint32_t g0 = 0; g0 < ngroups; g0 += BGV_FPW_THREADS) {
-    const uint32_t g = g0 + threadIdx.x;
-    bgv_dgroup G{};
-    bool fail = false;
-    if (g < ngroups) {
-      G = groups[g];
-      fail = !(verdict[g] & 1) && G.n_slots >= 2 && (G.flags & BGV_GROUP_SHARED);
-    }
-    const uint64_t bal = __ballot(fail);
-    if (lane == 0) wave_n[wave] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t off = base;
-    for (uint32_t w = 0; w < wave; ++w) off += wave_n[w];
-    uint32_t tot = 0;
-    for (uint32_t w = 0; w < BGV_FPW_THREADS / 64; ++w) tot += wave_n[w];
-    if (fail) {
-      const uint32_t i = off + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-      tg[i] = bgv_dgroup{G.first_slot, G.n_slots, BGV_ALL_SLOTS, g + 1, BGV_GROUP_WEIGHTED};
-      list[i] = g;
-    }
-    base += tot;
-    __syncthreads();  // wave_n is rewritten by the next chunk
-  }
-  if (threadIdx.x == 0) *count = base;
 }
 
 // The latency path's closing (small calls): one block of BGV_FOLD_TEAMS (16) teams per group.
@@ -373,7 +289,8 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
                        !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
-                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1, static_cast<const uint32_t*>(nullptr));
+                       b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1,
+                       !pairs && b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
   BGV_MARK(5);
   return hipGetLastError();
 }
@@ -399,34 +316,5 @@ hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, vo
   hipLaunchKernelGGL(k_final, dim3(1), dim3(64), 0, st, group, 1u, reinterpret_cast<const fp12_t*>(vals),
                      reinterpret_cast<const fp12_t*>(one), verdict, static_cast<fp12_t*>(nullptr),
                      static_cast<fp12_t*>(nullptr), static_cast<const fp12_t*>(nullptr));
-  return hipGetLastError();
-}
-
-// The first pass's weighted tests (bulk batches; bgv_api.cpp run_pass1): right after the
-// closing, on the same stream and with no host round trip, each failing group of the first
-// pass gets ONE test in which slot k enters with weight k + 1 -- its value
-// W = prod_k X_k^(k+1) against the group's V = prod_k X_k (X_k the slot's pairing value, 1 when
-// valid).  With exactly one invalid slot k, W = V^(k+1) and the closing finds w = k + 1 (V has
-// prime order r, so no other w <= 64 matches); the host then decides every job of the group
-// from the first pass.  Passing groups cost nothing: the failing ones are listed on the device
-// (k_fpw_list) and the tests' kernels run over that list (device count).
-//   1. k_fpw_list: tests tg[0, n) and their first-pass groups list[0, n) (n -> *dcount)
-//   2. bgv_launch_fpw_pairs (bgv_k_miller.hip): weighted signature sums and their pairs
-//   3. bgv_launch_fpw_close: k_final12 over the tests: prod_k f_k^(k+1) * pair, the final
-//      exponentiation, the identification against the first-pass u values (b.gu, intact: the
-//      tests write neither gu nor gprod); verdict bits 8..15 = w (0: none)
-hipError_t bgv_launch_fpw_list(const bgv_dev_batch& b, bgv_dgroup* tg, uint32_t* list, uint32_t* dcount,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(k_fpw_list, dim3(1), dim3(BGV_FPW_THREADS), 0, st, static_cast<const int32_t*>(b.verdict),
-                     b.ngroups, b.groups, tg, list, dcount);
-  return hipGetLastError();
-}
-hipError_t bgv_launch_fpw_close(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st) {
-  const uint32_t n_max = b.ngroups;
-  if (n_max == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_final12, dim3(nblk(n_max, BGV_FINAL12_TEAMS)), dim3(64), 0, st, tg, n_max,
-                     static_cast<const fp12_t*>(b.f), static_cast<const fp12_t*>(b.gpair + n_max), b.verdict + n_max,
-                     static_cast<fp12_t*>(nullptr),
-                     static_cast<fp12_t*>(nullptr), static_cast<const fp12_t*>(b.gu), dcount);
   return hipGetLastError();
 }

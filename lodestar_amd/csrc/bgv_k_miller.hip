@@ -53,47 +53,35 @@ __global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ g
 // S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an
 // infinity signature in the accumulator).  A team of 16 lanes per group: lane c sums
 // every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
-// dcount (nullable): the group count is min(ngroups, *dcount), known only on the device (the
-// first pass's weighted tests of its failing groups, bgv_launch_fpw); whole blocks past it exit.
+// A uniform first-pass group (BGV_GROUP_UNIFORM) also sums its live slots' r_i pk_i into
+// gpk: the group's set pairs are then one pair e(gpk, H) (the same slots k_facc would pair).
 __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                              const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
                                              const int32_t* __restrict__ sig_status,
                                              const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum,
-                                             const uint32_t* __restrict__ dcount) {
-  if (dcount) ngroups = min(ngroups, *dcount);
-  if (blockIdx.x * BGV_FINAL_TEAMS >= ngroups) return;
+                                             const g1_jac* __restrict__ rpk, g1_jac* __restrict__ gpk) {
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
   g2_jac acc = jac_infinity<fp2_t>();
-  if (!(g.flags & BGV_GROUP_WEIGHTED)) {
+  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+    if (!grp_has(g, k)) continue;
+    const uint32_t s = g.first_slot + k;
+    const int32_t ss = sig_status[s];
+    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+  }
+  if (gpk && (g.flags & BGV_GROUP_UNIFORM)) {  // uniform over the team
+    g1_jac pa = jac_infinity<fp_t>();
     for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
       if (!grp_has(g, k)) continue;
       const uint32_t s = g.first_slot + k;
-      const int32_t ss = sig_status[s];
-      if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+      if (slot_live(slots[s], sig_status[s], pk_status[s])) pa = jac_add(pa, rpk[s]);
     }
-  } else {
-    // sum_k (k + 1) R_k over this lane's slots k = c + 16 j: (c + 1) A + 16 B with A = sum_j R,
-    // B = sum_j j R (suffix sums, j descending); the butterfly below adds the lanes up
-    g2_jac A = jac_infinity<fp2_t>(), B = jac_infinity<fp2_t>();
-    for (int j = 3; j >= 0; --j) {
-      const uint32_t k = (uint32_t)c + BGV_TEAM * (uint32_t)j;
-      if (grp_has(g, k)) {
-        const uint32_t s = g.first_slot + k;
-        const int32_t ss = sig_status[s];
-        if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) A = jac_add(A, rsig[s]);
-      }
-      if (j >= 1) B = jac_add(B, A);
-    }
-    BGV_NO_UNROLL for (int t = 0; t < 4; ++t) B = jac_dbl(B);
-    const uint32_t w = (uint32_t)c + 1;
-    g2_jac T = jac_infinity<fp2_t>();
-    BGV_NO_UNROLL for (int bit = 4; bit >= 0; --bit) {
-      T = jac_dbl(T);
-      if ((w >> bit) & 1) T = jac_add(T, A);
-    }
-    acc = jac_add(T, B);
+    pa = jac_add(pa, point_xor<8>(pa));
+    pa = jac_add(pa, point_xor<4>(pa));
+    pa = jac_add(pa, point_xor<2>(pa));
+    pa = jac_add(pa, point_xor<1>(pa));
+    if (gi < ngroups && c == 0) gpk[gi] = pa;
   }
   acc = jac_add(acc, point_xor<8>(acc));
   acc = jac_add(acc, point_xor<4>(acc));
@@ -106,16 +94,13 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
 // pairs [nslots, nslots + ngroups) the groups' e(-G1, S_g).  The twist point runs the
 // generated rounds (bgv_tmiller_prog.h) on the team's LDS slots, the Fp12 accumulator is
 // coefficient-parallel.  Teams past the end (and pairs that take no part) compute on
-// zeros and store 1 or nothing, so every lane reaches every barrier.  dcount (nullable): the
-// group pairs are min(ngroups, *dcount) (as k_gsum's); whole blocks past the end exit.
+// zeros and store 1 or nothing, so every lane reaches every barrier.
 __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                                     const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
                                                     const int32_t* __restrict__ sig_status,
                                                     const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
                                                     uint32_t ngroups, const g2_jac* __restrict__ gsum,
-                                                    fp12_t* __restrict__ gpair, const uint32_t* __restrict__ dcount) {
-  if (dcount) ngroups = min(ngroups, *dcount);
-  if (blockIdx.x * BGV_FINAL_TEAMS >= nslots + ngroups) return;
+                                                    fp12_t* __restrict__ gpair) {
   __shared__ uint8_t prog[TMP_TABLE_BYTES];
   __shared__ fp_t S[BGV_FINAL_TEAMS][TMP_NSLOT];
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
@@ -328,8 +313,7 @@ static void launch_miller_latency(const bgv_dev_batch& b, uint32_t nslots, uint3
                        static_cast<fp12_t*>(nullptr));
   else
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(total, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, nslots, b.rpk,
-                       b.h, b.sig_status, b.pk_status, b.f, ngroups, b.gsum, b.gpair,
-                       static_cast<const uint32_t*>(nullptr));
+                       b.h, b.sig_status, b.pk_status, b.f, ngroups, b.gsum, b.gpair);
 }
 
 // lanes of one k_miller round: one wave of 64 on each SIMD (MI355X: 256 CUs x 4 SIMDs)
@@ -365,7 +349,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   }
   // the groups' signature sums, then set pairs and group pairs in one launch
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.groups, b.ngroups,
-                     b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const uint32_t*>(nullptr));
+                     b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk), b.gpk);
   BGV_MARK(2);
   const uint32_t R = miller_round_lanes();
   if (bgv_use_latency(b, n + b.ngroups)) {
@@ -375,8 +359,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
     // the group pairs on extra k_facc lanes would open one more round of one wave per SIMD
     // (131,072 sets + 2,048 groups: 3 rounds instead of 2); run them on teams instead
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, 0u,
-                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair,
-                       static_cast<const uint32_t*>(nullptr));
+                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
     if (bgv_single_pass_miller())
       hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
                          b.pk_status, b.f, 0u, b.gsum, b.gpair);
@@ -401,26 +384,10 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
-                     b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const uint32_t*>(nullptr));
+                     b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk), static_cast<g1_jac*>(nullptr));
   if (b.ngroups <= bgv_latency_max())
     launch_miller_latency(b, 0u, b.ngroups, st);
   else
     hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);
-  return hipGetLastError();
-}
-
-// The first pass's weighted tests (bgv_launch_fpw_list): the tests' signature sums and pairs,
-// over the groups [0, *dcount) of tg (each names its first-pass group in ref1), into gsum / gpair
-// past the first pass's b.ngroups entries.  Grids sized for b.ngroups tests; blocks past the
-// device count exit at once.
-hipError_t bgv_launch_fpw_pairs(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st) {
-  const uint32_t n_max = b.ngroups;
-  if (n_max == 0) return hipSuccess;
-  g2_jac* gsum = b.gsum + n_max;
-  fp12_t* gpair = b.gpair + n_max;
-  hipLaunchKernelGGL(k_gsum, dim3(nblk(n_max, BGV_FINAL_TEAMS)), dim3(64), 0, st, tg, n_max, b.slots, b.rsig,
-                     b.sig_status, b.pk_status, gsum, dcount);
-  hipLaunchKernelGGL(k_miller_team, dim3(nblk(n_max, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u, b.rpk, b.h,
-                     b.sig_status, b.pk_status, b.f, n_max, static_cast<const g2_jac*>(gsum), gpair, dcount);
   return hipGetLastError();
 }

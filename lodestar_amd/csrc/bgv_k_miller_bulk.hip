@@ -80,20 +80,36 @@ __global__ void BGV_KATTR_LINES k_lines(const bgv_dslot* __restrict__ slots, uin
 
 // Lanes [0, nslots): f_i over the records of the slot's signing root (slots[s].hsrc), 1 for a
 // slot that takes no part; lanes [nslots, nslots + ngroups): g_g = MillerLoop(-G1, S_g) (1 for
-// an infinite S_g).
+// an infinite S_g); lanes [nslots + ngroups, nslots + ngroups + npk): a uniform group's
+// (BGV_GROUP_UNIFORM) one set pair MillerLoop(gpk_g, H of its root) into gpkp_g.  The slots of
+// a uniform group take no lane of their own (their f_i stay unwritten: the closing multiplies
+// gpkp instead).  glist (nullable, *dcount first-pass groups: bgv_launch_uniform_refill): block
+// b computes the own pairs f_i of listed group glist[b]'s slots if it is uniform (the retry
+// tests multiply them), and nothing else.
 __global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                       const g1_jac* __restrict__ rpk, const int32_t* __restrict__ sig_status,
                                       const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ lines,
                                       uint32_t cap, fp12_t* __restrict__ f, uint32_t ngroups,
-                                      const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+                                      const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair,
+                                      const bgv_dgroup* __restrict__ groups, uint32_t npk,
+                                      const g1_jac* __restrict__ gpk, fp12_t* __restrict__ gpkp,
+                                      const uint32_t* __restrict__ glist, const uint32_t* __restrict__ dcount) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (glist) {  // refill: the slots of one listed uniform group per block
+    if (blockIdx.x >= *dcount) return;
+    const bgv_dgroup G = groups[glist[blockIdx.x]];
+    if (!(G.flags & BGV_GROUP_UNIFORM) || threadIdx.x >= G.n_slots) return;
+    s = G.first_slot + threadIdx.x;
+  }
   bool live;
   uint32_t lp;
   const g1_jac* P;
   fp12_t* out;
   if (s < nslots) {
-    live = slot_live(slots[s], sig_status[s], pk_status[s]);
-    lp = slots[s].hsrc;
+    const bgv_dslot& d = slots[s];
+    if (!glist && groups && !(d.flags & BGV_SLOT_PAD) && (groups[d.group].flags & BGV_GROUP_UNIFORM)) return;
+    live = slot_live(d, sig_status[s], pk_status[s]);
+    lp = d.hsrc;
     P = rpk + s;
     out = f + s;
   } else if (s - nslots < ngroups) {
@@ -102,6 +118,14 @@ __global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint3
     lp = nslots + g;
     P = &kNegG1JacB;
     out = gpair + g;
+  } else if (s - nslots - ngroups < npk) {
+    const uint32_t g = s - nslots - ngroups;
+    const bgv_dgroup G = groups[g];
+    if (!(G.flags & BGV_GROUP_UNIFORM)) return;
+    live = !jac_is_inf(gpk[g]);
+    lp = slots[G.first_slot].hsrc;
+    P = gpk + g;
+    out = gpkp + g;
   } else {
     return;
   }
@@ -150,15 +174,31 @@ uint32_t bgv_lines_pairs(const bgv_dev_batch& b) {
 }
 size_t bgv_line_record_bytes() { return (size_t)BGV_MILLER_STEPS * BGV_LINE_WORDS * 4; }
 
-// the set pairs [0, nslots) and the group pairs [nslots, nslots + ngroups) of a bulk batch;
-// ngroups = 0 when the group pairs run on teams instead (bgv_launch_miller)
+// the set pairs [0, nslots), the group pairs [nslots, nslots + ngroups) and, with uniform
+// groups (b.uniform), their pubkey-sum pairs of a bulk batch; ngroups = 0 when the group pairs
+// run on teams instead (bgv_launch_miller)
 hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipStream_t st) {
   if (!b.lines || b.lines_cap < b.nslots + ngroups) return hipErrorInvalidValue;
   const uint32_t nq = b.uniq ? b.nuniq : b.nslots;
+  const uint32_t npk = b.uniform ? b.ngroups : 0u;
   if (nq + ngroups)
     hipLaunchKernelGGL(k_lines, dim3(nblk(nq + ngroups, 64)), dim3(64), 0, st, b.slots, b.nslots, b.h, b.uniq, nq,
                        ngroups, b.gsum, b.lines, b.lines_cap);
-  hipLaunchKernelGGL(k_facc, dim3(nblk(b.nslots + ngroups, 64)), dim3(64), 0, st, b.slots, b.nslots, b.rpk,
-                     b.sig_status, b.pk_status, b.lines, b.lines_cap, b.f, ngroups, b.gsum, b.gpair);
+  hipLaunchKernelGGL(k_facc, dim3(nblk(b.nslots + ngroups + npk, 64)), dim3(64), 0, st, b.slots, b.nslots, b.rpk,
+                     b.sig_status, b.pk_status, b.lines, b.lines_cap, b.f, ngroups, b.gsum, b.gpair,
+                     b.uniform ? b.groups : nullptr, npk, static_cast<const g1_jac*>(b.gpk), b.gpkp,
+                     static_cast<const uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr));
+  return hipGetLastError();
+}
+
+// The own pairs f_i of the slots of the listed uniform first-pass groups (glist[0, *dcount) <=
+// b.ngroups), for the retry tests; one block per listed group.
+hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,
+                                     hipStream_t st) {
+  if (b.ngroups == 0) return hipSuccess;
+  if (!b.lines) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_facc, dim3(b.ngroups), dim3(64), 0, st, b.slots, b.nslots, b.rpk, b.sig_status, b.pk_status,
+                     b.lines, b.lines_cap, b.f, 0u, b.gsum, b.gpair, b.groups, 0u,
+                     static_cast<const g1_jac*>(b.gpk), b.gpkp, glist, dcount);
   return hipGetLastError();
 }

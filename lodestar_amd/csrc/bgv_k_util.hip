@@ -204,7 +204,7 @@ static size_t fsig_slots(uint32_t cap_slots) { return std::min<size_t>(cap_slots
 size_t bgv_slot_mem_bytes(uint32_t cap_slots) {
   return bgv_slot_bytes() * (size_t)cap_slots + sizeof(fp12_t) * fsig_slots(cap_slots);
 }
-size_t bgv_group_bytes() { return sizeof(g2_jac) + 3 * sizeof(fp12_t) + sizeof(int32_t); }
+size_t bgv_group_bytes() { return sizeof(g2_jac) + 4 * sizeof(fp12_t) + sizeof(g1_jac) + sizeof(int32_t); }
 size_t bgv_cache_entry_bytes() { return sizeof(g1_aff); }
 
 void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group_mem, uint32_t cap_groups) {
@@ -233,6 +233,10 @@ void bgv_carve(bgv_dev_batch* b, void* slot_mem, uint32_t cap_slots, void* group
   q += sizeof(fp12_t) * (size_t)cap_groups;
   b->gu = reinterpret_cast<fp12_t*>(q);
   q += sizeof(fp12_t) * (size_t)cap_groups;
+  b->gpkp = reinterpret_cast<fp12_t*>(q);
+  q += sizeof(fp12_t) * (size_t)cap_groups;
+  b->gpk = reinterpret_cast<g1_jac*>(q);
+  q += sizeof(g1_jac) * (size_t)cap_groups;
   b->verdict = reinterpret_cast<int32_t*>(q);
 }
 

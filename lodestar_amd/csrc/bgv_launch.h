@@ -28,6 +28,7 @@ struct bgv_cache_entry;
 struct bgv_dev_batch {
   uint32_t nslots, ngroups;
   uint32_t max_npk;  // largest n_pk of any slot (k_pk_agg runs only when a set reaches BGV_PK_TREE_MIN)
+  bool uniform;      // some group carries BGV_GROUP_UNIFORM (bulk first passes only)
   int path;          // BGV_PATH_AUTO by size, BGV_PATH_BULK / BGV_PATH_LATENCY forced (bgv_debug_prepare)
   // slots whose H(msg) the bulk k_prep computes (the first slot of each distinct signing root of
   // a call); the other slots read H at their hsrc.  Null: every slot hashes its own message.
@@ -49,6 +50,8 @@ struct bgv_dev_batch {
   int32_t* pk_status;
   jac_t<fp2_t>* gsum;  // per group: sum of its r_i sig_i
   fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
+  jac_t<fp_t>* gpk;    // per uniform group (BGV_GROUP_UNIFORM): sum of its live r_i pk_i
+  fp12_t* gpkp;        // per uniform group: MillerLoop(gpk, H of the group's root)
   fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
   fp12_t* gu;          // per group: u = gprod^((p^2+1) 3 (p^4-p^2+1)/r); pairing value conj(u)/u
   // retry rounds with pattern tests: the first pass's u values (a copy of its gu), indexed by
@@ -88,18 +91,14 @@ uint32_t bgv_lines_pairs(const bgv_dev_batch& b);  // line records the batch nee
 bool bgv_single_pass_miller();                     // BGV_MILLER_1PASS: k_miller instead (A/B)
 size_t bgv_line_record_bytes();                    // bytes of one pair's 68 records
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs);
-// bgv_launch_groups closes with k_final12 (which takes BGV_GROUP_WEIGHTED tests) iff
+// bgv_launch_groups closes with k_final12 iff
 // nslots + ngroups exceeds this (else k_final_fold)
 uint32_t bgv_fold_pairs_max();
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
-// The first pass's weighted tests of its failing groups (bulk batches, after bgv_launch_groups
-// on the same stream; bgv_k_final.hip): list (tg / list / *dcount, at most b.ngroups), pairs,
-// closing.  tg and the tests' sums, pairs and verdicts are the entries [b.ngroups, 2 b.ngroups)
-// of the group arrays (the Exec reserves twice the groups).
-hipError_t bgv_launch_fpw_list(const bgv_dev_batch& b, bgv_dgroup* tg, uint32_t* list, uint32_t* dcount,
-                               hipStream_t st);
-hipError_t bgv_launch_fpw_pairs(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st);
-hipError_t bgv_launch_fpw_close(const bgv_dev_batch& b, const bgv_dgroup* tg, const uint32_t* dcount, hipStream_t st);
+// the own set pairs f_i of the slots of listed uniform first-pass groups (glist[0, *dcount),
+// device memory; bgv_k_miller_bulk.hip; needs the first pass's line records and groups)
+hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,
+                                     hipStream_t st);
 size_t bgv_slot_bytes();
 size_t bgv_slot_mem_bytes(uint32_t cap_slots);  // the per-slot arrays of an Exec of cap_slots slots
 size_t bgv_group_bytes();

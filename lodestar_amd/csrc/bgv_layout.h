@@ -41,11 +41,6 @@ enum {
 // names the first-pass group (index ref1 - 1 of the batch) whose pairing value this group's
 // is compared with: the closing then also reports whether the two values agree, i.e. whether
 // the rest of that group (its complement) passes (verdict bit 1).
-// flags & BGV_GROUP_WEIGHTED (a retry round's weighted test of a failing first-pass group
-// ref1 - 1, bgv_api.cpp): slot k of the group enters with weight k + 1 -- the closing multiplies
-// prod_k f_k^(k+1) * e(-G1, sum_k (k+1) r_k sig_k) (k_gsum, k_final12) -- and reports the weight
-// w in 1..n_slots with (pairing value of ref1 - 1)^w == this group's value, or 0, in verdict
-// bits 8..15: with exactly one invalid slot k that is k + 1.
 struct bgv_dgroup {
   uint32_t first_slot;  // multiple of BGV_WAVE
   uint32_t n_slots;     // 1..64
@@ -54,7 +49,9 @@ struct bgv_dgroup {
   uint32_t flags;
 };
 #define BGV_ALL_SLOTS (~0ull)
-#define BGV_GROUP_WEIGHTED 1u
-// a first-pass group shared by several batchable jobs (only such a group is retried per job,
-// so only its failure takes the first pass's weighted test, bgv_launch_fpw_list)
-#define BGV_GROUP_SHARED 2u
+// flags: a first-pass group of a bulk batch whose sets all share one signing root (slot
+// first_slot's hsrc) and whose jobs lie inside it.  prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H),
+// so the group's set pairs are ONE Miller loop over its pubkey sum (k_gsum -> gpk, k_facc ->
+// gpkp) and its slots take none; when such a group fails, the retry thread first computes its
+// slots' own pairs for the retry tests (bgv_launch_uniform_refill)
+#define BGV_GROUP_UNIFORM 4u

@@ -90,14 +90,14 @@ def test_split_min_one_acts_as_two(ctxs):
 
 
 # ---------------------------------------------------------------------------------------
-# The first pass's weighted tests (bgv_launch_fpw_*, bgv_api.cpp call_after_pass1): every failing
-# shared group of a bulk batch takes one weighted test right after the closing; a group with one
-# invalid slot is decided from the first pass.  Multi-set batchable jobs: a job inside one group
-# is identified by its slot; jobs that straddle two groups are not pattern-eligible and keep the
-# retry rounds.  Every verdict must equal the job verified alone (BGV_MODE_PER_JOB;
-# chain/bls/multithread/worker.ts:76-98).
+# Retry of multi-set batchable jobs in a bulk call: jobs inside one group take the pattern
+# tests, jobs that straddle two groups the fanout bisection, one job holding two invalid sets,
+# three invalid jobs in one group.  Every verdict must equal the job verified alone
+# (BGV_MODE_PER_JOB; chain/bls/multithread/worker.ts:76-98).  (Round 5 measured a weighted test
+# per failing group in the first pass itself -- equal or slower at the headline, profiles/r05/
+# fpw_ab/ -- and dropped it.)
 # ---------------------------------------------------------------------------------------
-def test_first_pass_weighted_tests_multi_set_jobs(ctxs):
+def test_retry_multi_set_jobs_bulk(ctxs):
     from lodestar_amd import native
     (one, _), sks = ctxs
     n = 6000 * 3  # 18,000 sets > BGV_LATENCY_MAX: a bulk batch
@@ -117,3 +117,62 @@ def test_first_pass_weighted_tests_multi_set_jobs(ctxs):
     assert got == want
     assert sum(1 for v in got if v != 1) == 9  # ten wrong sets, two of them in one job
     assert st.batch_retries >= 6
+
+
+# ---------------------------------------------------------------------------------------
+# Uniform groups (BGV_GROUP_UNIFORM): in a bulk call the batchable one-set jobs are laid out
+# grouped by signing root, and a group whose sets all share one root takes ONE Miller loop over
+# its pubkey sum, e(sum_i r_i pk_i, H) = prod_i e(r_i pk_i, H), instead of one per set; a failing
+# uniform group gets its slots' own pairs for the retry tests.  Gossip attestations of one
+# committee share a root (SURVEY 8(d) "mainnet-shaped").  Every verdict must equal the job
+# verified alone (chain/bls/multithread/worker.ts:76-98).
+# ---------------------------------------------------------------------------------------
+def test_uniform_groups_interleaved_committees(ctxs):
+    from lodestar_amd import native
+    (one, _), sks = ctxs
+    n = 24000
+    ncomm = 40  # committees, interleaved in arrival order: the layout regroups them by root
+    comm = [(i * 7) % ncomm for i in range(n)]
+    roots = [hashlib.sha256(b"r05-uniform-%d" % c).digest() for c in range(ncomm)]
+    keys = [(i * 13) % NKEYS for i in range(n)]
+    msgs = [roots[c] for c in comm]
+    sigs = one.sign(b"".join(sks[k] for k in keys), b"".join(msgs))
+    sets = [native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=[keys[i]]) for i in range(n)]
+    want = [1] * n
+    # wrong keys keep their committee's root (their uniform group fails and is retried):
+    # singles, two in one committee close together, and one beside an undecodable signature;
+    # a wrong message is a root of its own
+    for i in (3, 4000, 4040, 12345, 23999, 777):
+        sets[i] = native.SetSpec(msgs[i], sets[i].sig, pk_indices=[(keys[i] + 1) % NKEYS])
+        want[i] = 0
+    sets[778] = native.SetSpec(msgs[778], bytes([sets[778].sig[0] & 0x7F]) + sets[778].sig[1:], pk_indices=[keys[778]])
+    want[778] = -native.BLST_BAD_ENCODING
+    sets[9000] = native.SetSpec(hashlib.sha256(b"other").digest(), sets[9000].sig, pk_indices=[keys[9000]])
+    want[9000] = 0
+    jobs = [([s], True) for s in sets]
+    # a multi-set batchable job and a non-batchable 64-set job ride along
+    extra = [(sets[100:103], True), (sets[200:264], False)]
+    st = native.BgvStats()
+    got = one.verify_jobs(jobs + extra, native.MODE_WORKER, stats=st)
+    assert got[:n] == want
+    assert got[n:] == [1, 1]
+    assert st.batch_retries >= 5
+    # the same sets one by one (small calls: the latency path, no uniform groups)
+    assert one.verify_jobs(jobs[:64], native.MODE_PER_JOB) == want[:64]
+
+
+def test_uniform_groups_one_job(ctxs):
+    """One non-batchable job of 8192 sets over 16 roots (the epoch sweep's shape): uniform groups
+    inside one job; valid, and false with one wrong key."""
+    from lodestar_amd import native
+    (one, two), sks = ctxs
+    n = 8192
+    roots = [hashlib.sha256(b"r05-sweep-%d" % (i // 512)).digest() for i in range(n)]
+    sigs = one.sign(b"".join(sks[i % NKEYS] for i in range(n)), b"".join(roots))
+    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[i % NKEYS]) for i in range(n)]
+    for c in (one, two):
+        assert c.verify_jobs([(sets, False)], native.MODE_WORKER) == [1]
+    bad = list(sets)
+    bad[5000] = native.SetSpec(roots[5000], sets[5000].sig, pk_indices=[(5000 + 1) % NKEYS])
+    for c in (one, two):
+        assert c.verify_jobs([(bad, False)], native.MODE_WORKER) == [0]

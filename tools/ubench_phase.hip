@@ -71,6 +71,33 @@ __global__ void KATTR k_glv1(const g1_jac* __restrict__ in, const uint64_t* __re
   if (s < n) out[s] = jac_mul_glv(in[s], k[s]);
 }
 
+// hash_to_G2 without the cofactor clearing: XMD, the two SSWU maps, the isogeny, their sum
+__global__ void KATTR k_hmap(const uint8_t* __restrict__ msgs, g2_jac* __restrict__ out, uint32_t n) {
+  stamp_scope st;
+  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  if (s >= n) return;
+  uint8_t m[32];
+  for (int i = 0; i < 32; ++i) m[i] = msgs[32 * s + i];
+  fp2_t u0, u1;
+  hash_to_field_fp2(&u0, &u1, m, 32);
+  const fp_t sm5 = fp_sqrt_minus5();
+  const g2_jac q0 = iso_map_g2_jac(sswu_g2_jac(u0, sm5));
+  const g2_jac q1 = iso_map_g2_jac(sswu_g2_jac(u1, sm5));
+  out[s] = jac_add(q0, q1);
+}
+// one SSWU map to Jacobian (its square-root exponentiation included), no isogeny
+__global__ void KATTR k_sswu(const g2_jac* __restrict__ in, g2_jac* __restrict__ out, uint32_t n) {
+  stamp_scope st;
+  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  if (s < n) out[s] = sswu_g2_jac(in[s].x, fp_sqrt_minus5());
+}
+// the Fp exponentiation (p-3)/4 alone
+__global__ void KATTR k_pow(const g2_jac* __restrict__ in, g2_jac* __restrict__ out, uint32_t n) {
+  stamp_scope st;
+  const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+  if (s < n) out[s].x.c0 = fp_pow_fixed<BGV_POW_P34>(in[s].x.c0);
+}
+
 static uint32_t rnd(uint64_t* x) {
   *x ^= *x << 13;
   *x ^= *x >> 7;
@@ -112,6 +139,14 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&d1, sizeof(g1_jac) * n));
   CHECK(hipMalloc(&o1, sizeof(g1_jac) * n));
   CHECK(hipMalloc(&dk, 8 * n));
+  uint8_t* dm;
+  CHECK(hipMalloc(&dm, 32 * n));
+  {
+    uint8_t* hm = new uint8_t[32 * n];
+    for (uint32_t i = 0; i < 32 * n; ++i) hm[i] = (uint8_t)rnd(&x);
+    CHECK(hipMemcpy(dm, hm, 32 * n, hipMemcpyHostToDevice));
+    delete[] hm;
+  }
   CHECK(hipMemcpy(d2, h2, sizeof(g2_jac) * n, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(d1, h1, sizeof(g1_jac) * n, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(dk, hk, 8 * n, hipMemcpyHostToDevice));
@@ -174,6 +209,12 @@ int main(int argc, char** argv) {
     if (timeit("glv2", [&] { hipLaunchKernelGGL(k_glv2, grid, dim3(64), 0, 0, d2, dk, o2, n); }, sum2)) return 1;
   if (all || !strcmp(only, "glv1"))
     if (timeit("glv1", [&] { hipLaunchKernelGGL(k_glv1, grid, dim3(64), 0, 0, d1, dk, o1, n); }, sum1)) return 1;
+  if (all || !strcmp(only, "hmap"))
+    if (timeit("hmap", [&] { hipLaunchKernelGGL(k_hmap, grid, dim3(64), 0, 0, dm, o2, n); }, sum2)) return 1;
+  if (all || !strcmp(only, "sswu"))
+    if (timeit("sswu", [&] { hipLaunchKernelGGL(k_sswu, grid, dim3(64), 0, 0, d2, o2, n); }, sum2)) return 1;
+  if (all || !strcmp(only, "pow"))
+    if (timeit("pow", [&] { hipLaunchKernelGGL(k_pow, grid, dim3(64), 0, 0, d2, o2, n); }, sum2)) return 1;
   if (all || !strcmp(only, "cof"))
     if (timeit("cof", [&] { hipLaunchKernelGGL(k_cof, grid, dim3(64), 0, 0, d2, o2, n); }, sum2)) return 1;
   return 0;
