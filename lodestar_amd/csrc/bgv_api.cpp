@@ -1576,9 +1576,14 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
               hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
     int least = 0, greatest = 0;
     ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+    // BGV_RETRY_PRIO=0: the retry streams at normal priority (A/B measurements)
+    static const bool retry_high = [] {
+      const char* e = getenv("BGV_RETRY_PRIO");
+      return !(e && atoi(e) == 0);
+    }();
     for (int k = 0; ok && k < retry_threads_per_device(); ++k) {
       hipStream_t st = nullptr;
-      ok = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest) == hipSuccess;
+      ok = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, retry_high ? greatest : least) == hipSuccess;
       if (ok) d.sched->retries.push_back(st);
     }
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {

@@ -9,6 +9,8 @@
 #   driver   the headline window with the driver's step counts (--steps 20 --warmup 5) and with
 #            the default ones (64 / 16), back to back                 -> OUTDIR/bench_steps.jsonl (appends)
 #   trace    rocprofv3 --kernel-trace --stats of the bench command   -> OUTDIR/bench_trace/
+#   retrytrace  kernel traces of the headline window with 1 % corrupted sets and with none, and
+#            one BGV_TRACE run of the corrupted window (its retry rounds)   -> OUTDIR/retry_{c1,c0}/, retry_trace.err
 #   roof     rocprofv3 --kernel-trace --stats of the isolated roofline call -> OUTDIR/roof_trace/
 #   pmc      the PMC passes of the roofline call (tools/gpu/pmc.sh)  -> gpurun_out/<basename OUTDIR>/pmc
 #   latency  config-3 latency probe under a kernel trace              -> OUTDIR/config3_p50.json, lat_trace/
@@ -49,6 +51,15 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/bench_trace" -o run --output-format csv \
         -- python3 bench.py --no-cpu-baseline > "$O/bench_traced.json" 2> "$O/bench_traced.err" \
         || fail trace $? "$O/bench_traced.err" ;;
+    retrytrace)
+      for c in 1 0; do
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/retry_c$c" -o run --output-format csv \
+          -- python3 bench.py --no-cpu-baseline --no-block-import --no-epoch-sweep --corrupt 0.0$c \
+          > "$O/retry_c$c.json" 2> "$O/retry_c$c.err" || fail retrytrace $? "$O/retry_c$c.err"
+      done
+      BGV_TRACE=1 timeout -k 10 150 python bench.py --no-cpu-baseline --no-block-import --no-epoch-sweep \
+        > "$O/retry_trace.json" 2> "$O/retry_trace.err" || fail retrytrace $? "$O/retry_trace.err"
+      cat "$O"/retry_c*.json | python tools/gpu/summarize.py - ;;
     roof)
       timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/roof_trace" -o run --output-format csv \
         -- python3 tools/gpu/roof_call.py > "$O/roof_call.json" 2> "$O/roof_call.err" \
