@@ -199,11 +199,12 @@ def make_gossip_batch(ctx, native, rank, nsets, nkeys, corrupt_frac=0.01, seed=0
     return jobs, expect, key_of
 
 
-def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, steps=64, warmup=16, settle_s=0.6):
+def mainnet_shaped_throughput(ctx, native, nkeys, nsets=8192, committee=128, steps=64, warmup=16, settle_s=0.6,
+                              corrupt=0.01):
     """config 4 with mainnet-shaped signing roots (one per 128-set committee):
     the same streaming window as the headline; k_prep hashes each distinct root of a call
     once (bgv_dslot.hsrc), so per-set work drops by most of hash_to_G2."""
-    jobs, expect, _ = make_gossip_batch(ctx, native, 0, nsets, nkeys, committee=committee)
+    jobs, expect, _ = make_gossip_batch(ctx, native, 0, nsets, nkeys, corrupt_frac=corrupt, committee=committee)
     packed = native.PackedCall(jobs)
 
     def step():

@@ -109,9 +109,6 @@ static int execs_per_device() {
   return std::max(v, dispatchers_per_device());
 }
 
-// Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
-// retry rounds of several super-batches then run side by side instead of queueing behind one
-// another (their rounds are latency-bound chains of small launches)
 // BGV_UNIFORM=0 turns off uniform groups (BGV_GROUP_UNIFORM: one Miller loop per group whose sets
 // share a signing root, and the grouping of a call's batchable one-set jobs by root that makes
 // them), for A/B measurements; on by default
@@ -125,6 +122,9 @@ static bool uniform_enabled() {
 // calls with fewer batchable one-set jobs take the latency path: their jobs keep their order
 #define BGV_UNIFORM_MIN_JOBS 1024
 
+// Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
+// retry rounds of several super-batches then run side by side instead of queueing behind one
+// another (their rounds are latency-bound chains of small launches)
 static int retry_threads_per_device() {
   static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
   return v;
@@ -1353,6 +1353,8 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     int32_t* rv = x.h_verdict.p;
     HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
     b = make_batch(d, x, nslots, nrg);
+    b.lines = x.d_lines;  // free after the first pass (and the refill): the tests' line records
+    b.lines_cap = x.lines_cap;
     bool pattern = false;
     for (Call* call : calls) pattern = pattern || !call->punits.empty();
     if (pattern) b.gu1 = x.d_gu1;

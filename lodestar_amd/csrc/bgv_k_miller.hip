@@ -95,12 +95,12 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
 // generated rounds (bgv_tmiller_prog.h) on the team's LDS slots, the Fp12 accumulator is
 // coefficient-parallel.  Teams past the end (and pairs that take no part) compute on
 // zeros and store 1 or nothing, so every lane reaches every barrier.
-__global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict__ slots, uint32_t nslots,
-                                                    const g1_jac* __restrict__ rpk, const g2_jac* __restrict__ h,
-                                                    const int32_t* __restrict__ sig_status,
-                                                    const int32_t* __restrict__ pk_status, fp12_t* __restrict__ f,
-                                                    uint32_t ngroups, const g2_jac* __restrict__ gsum,
-                                                    fp12_t* __restrict__ gpair) {
+#define BGV_MTEAM_ARGS                                                                                      \
+  const bgv_dslot *__restrict__ slots, uint32_t nslots, const g1_jac *__restrict__ rpk,                      \
+      const g2_jac *__restrict__ h, const int32_t *__restrict__ sig_status, const int32_t *__restrict__ pk_status, \
+      fp12_t *__restrict__ f, uint32_t ngroups, const g2_jac *__restrict__ gsum, fp12_t *__restrict__ gpair
+}  // extern "C"
+__device__ __forceinline__ void miller_team_body(BGV_MTEAM_ARGS) {
   __shared__ uint8_t prog[TMP_TABLE_BYTES];
   __shared__ fp_t S[BGV_FINAL_TEAMS][TMP_NSLOT];
   __shared__ fp_t lds[BGV_FINAL_TEAMS][2 * BGV_TEAM_COMPS];
@@ -177,6 +177,10 @@ __global__ void __launch_bounds__(64) k_miller_team(const bgv_dslot* __restrict_
     fp12_t* dst = set_pair ? f + uu : gpair + (uu - nslots);
     reinterpret_cast<fp_t*>(dst)[tm_fp_index(cc)] = live ? x : (cc == 0 ? fp_one() : fp_zero());
   }
+}
+extern "C" {
+__global__ void __launch_bounds__(64) k_miller_team(BGV_MTEAM_ARGS) {
+  miller_team_body(slots, nslots, rpk, h, sig_status, pk_status, f, ngroups, gsum, gpair);
 }
 
 // The same pairs with one pair per block for the smallest calls, on two waves that run the
@@ -385,7 +389,10 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk), static_cast<g1_jac*>(nullptr));
-  if (b.ngroups <= bgv_latency_max())
+  const uint32_t lanes_min = bgv_retry_lanes_min();
+  if (lanes_min && b.ngroups >= lanes_min && b.lines && b.lines_cap >= b.ngroups && !bgv_single_pass_miller()) {
+    if (hipError_t e = bgv_launch_gpairs_bulk(b, st); e != hipSuccess) return e;
+  } else if (b.ngroups <= bgv_latency_max())
     launch_miller_latency(b, 0u, b.ngroups, st);
   else
     hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);

@@ -19,14 +19,16 @@ def main():
     ap.add_argument("repeats", type=int, nargs="?", default=2)
     ap.add_argument("--nkeys", type=int, default=131072)
     ap.add_argument("--committee", type=int, default=128)
+    ap.add_argument("--corrupt", type=float, default=0.01)
     args = ap.parse_args()
     from lodestar_amd import native
     ctx = native.Context([0])
     ctx.keygen(b"".join(bench.interop_sk(i) for i in range(args.nkeys)), cache_first=0, want_pubkeys=False)
     knobs = {k: v for k, v in os.environ.items() if k.startswith("BGV_")}
     for _ in range(args.repeats):
-        r = bench.mainnet_shaped_throughput(ctx, native, args.nkeys, committee=args.committee)
-        print(json.dumps({"mainnet_shaped": r["value"], "committee": args.committee, "env": knobs}), flush=True)
+        r = bench.mainnet_shaped_throughput(ctx, native, args.nkeys, committee=args.committee, corrupt=args.corrupt)
+        print(json.dumps({"mainnet_shaped": r["value"], "committee": args.committee, "corrupt": args.corrupt,
+                          "env": knobs}), flush=True)
     ctx.close()
 
 

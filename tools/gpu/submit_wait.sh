@@ -7,8 +7,8 @@ LOG=$1; TMO=$2; shift 2
 for i in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout "$TMO" -- "$@" > "$LOG" 2>&1
   rc=$?
-  [ $rc -ne 3 ] && exit $rc
-  grep -q "slot(s) on this pod are busy\|no box" "$LOG" || exit $rc
+  [ $rc -eq 0 ] && exit 0
+  grep -q "slot(s) on this pod are busy\|no box\|no free box\|retry in a few minutes" "$LOG" || exit $rc
   sleep 180
 done
 exit 3
