@@ -1353,8 +1353,6 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     int32_t* rv = x.h_verdict.p;
     HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
     b = make_batch(d, x, nslots, nrg);
-    b.lines = x.d_lines;  // free after the first pass (and the refill): the tests' line records
-    b.lines_cap = x.lines_cap;
     bool pattern = false;
     for (Call* call : calls) pattern = pattern || !call->punits.empty();
     if (pattern) b.gu1 = x.d_gu1;

@@ -93,27 +93,6 @@ static inline uint32_t bgv_latency_max() {
   return v;
 }
 
-// Retry rounds of a bulk batch with at least BGV_RETRY_LANES tests run their test pairs
-// MillerLoop(-G1, S_t) one per lane through k_lines + k_facc (the first pass's line-record
-// buffer, whose slot records the rounds no longer read), and with at least BGV_RETRY_LANE_CLOSE
-// tests their closings one per lane (k_final_lane), instead of on 12-lane teams: a fraction of
-// the SIMD time per test (a team spends 12 lanes for ~3 ms on a pair one lane does in ~11 ms).
-// Off by default (0): measured, the headline fell from 2.42-2.44 to 1.94-2.03 M sets/s with the
-// per-lane pairs (profiles/r05/retry_lanes/) -- the retry stream's one-wave-per-SIMD launches
-// wait on the first passes' waves for whole SIMDs.
-static inline uint32_t bgv_env_u32(const char* name, uint32_t dflt) {
-  const char* e = getenv(name);
-  return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
-}
-static inline uint32_t bgv_retry_lanes_min() {
-  static const uint32_t v = bgv_env_u32("BGV_RETRY_LANES", 0);
-  return v;
-}
-static inline uint32_t bgv_retry_lane_close_min() {
-  static const uint32_t v = bgv_env_u32("BGV_RETRY_LANE_CLOSE", 0);
-  return v;
-}
-
 // the latency path's kernels for this batch: forced by b.path, else by size
 static inline bool bgv_use_latency(const bgv_dev_batch& b, uint32_t pairs) {
   return b.path == BGV_PATH_LATENCY || (b.path == BGV_PATH_AUTO && pairs <= bgv_latency_max());

@@ -129,39 +129,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   final12_body(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, gpkp);
 }
 
-// A retry round's closing one test per lane (bgv_retry_lane_close_min): v = g_t * prod f_i over the
-// test's slots, then blst's final exponentiation F = v^(3 (p^12 - 1) / r) on the lane (easy part
-// with one Fp12 inversion, so the hard part squares in the cyclotomic subgroup: bls_pairing.h
-// final_exp).  Verdict bits as verdict_bits: bit 0 F = 1; bit 1 F equals the value of the
-// first-pass group ref1 - 1, whose k_final12 u gives F_ref = conj(u) / u, so F = F_ref iff
-// F u = conj(u) (no inversion).  The lanes of a wave loop to their longest slot list.
-__global__ void BGV_KATTR k_final_lane(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
-                                       const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
-                                       int32_t* __restrict__ verdict, const fp12_t* __restrict__ gu1) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ngroups) return;
-  const bgv_dgroup g = groups[t];
-  uint64_t m = g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1));
-  fp12_t x = gpair[t];
-  while (m) {
-    const int k = __ffsll((unsigned long long)m) - 1;
-    m &= m - 1;
-    x = fp12_mul(x, f[g.first_slot + k]);
-  }
-  const fp12_t F = final_exp(x);
-  int32_t v = fp12_is_one(F) ? 1 : 0;
-  if (gu1 && g.ref1) {
-    const fp12_t ur = gu1[g.ref1 - 1];
-    const fp12_t l = fp12_mul(F, ur), r = fp12_conj(ur);
-    bool eq = true;
-    const fp2_t* a = &l.c0.c0;
-    const fp2_t* b = &r.c0.c0;
-    for (int i = 0; i < 6; ++i) eq = eq && fp2_eq(a[i], b[i]);
-    if (eq) v |= 2;
-  }
-  verdict[t] = v;
-}
-
 // The latency path's closing (small calls): one block of BGV_FOLD_TEAMS (16) teams per group.
 // Team t multiplies the group's slots t, t + 16, ... (team 0 also the signature pair), the
 // partial products meet in LDS in a four-level tree (a sixteenth of k_final's serial product
@@ -323,11 +290,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     const char* e = getenv("BGV_FOLD_LEAN");
     return !(e && atoi(e) == 0);
   }();
-  const uint32_t lanes_min = bgv_retry_lane_close_min();
-  if (pairs && lanes_min && b.ngroups >= lanes_min && b.nslots + b.ngroups > bgv_latency_max())
-    hipLaunchKernelGGL(k_final_lane, dim3(nblk(b.ngroups, 64)), dim3(64), 0, s.main, b.groups, b.ngroups, b.f,
-                       b.gpair, b.verdict, b.gu1);
-  else if (b.nslots + b.ngroups <= bgv_latency_max())
+  if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,

@@ -389,10 +389,7 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk), static_cast<g1_jac*>(nullptr));
-  const uint32_t lanes_min = bgv_retry_lanes_min();
-  if (lanes_min && b.ngroups >= lanes_min && b.lines && b.lines_cap >= b.ngroups && !bgv_single_pass_miller()) {
-    if (hipError_t e = bgv_launch_gpairs_bulk(b, st); e != hipSuccess) return e;
-  } else if (b.ngroups <= bgv_latency_max())
+  if (b.ngroups <= bgv_latency_max())
     launch_miller_latency(b, 0u, b.ngroups, st);
   else
     hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);

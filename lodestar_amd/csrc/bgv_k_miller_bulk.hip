@@ -191,21 +191,6 @@ hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipS
   return hipGetLastError();
 }
 
-// A retry round's group pairs g_t = MillerLoop(-G1, S_t), t < b.ngroups, one per lane: the
-// records of pair t at index t (no set pairs: nslots = 0 in both launches).
-hipError_t bgv_launch_gpairs_bulk(const bgv_dev_batch& b, hipStream_t st) {
-  if (b.ngroups == 0) return hipSuccess;
-  if (!b.lines || b.lines_cap < b.ngroups) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lines, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.slots, 0u, b.h,
-                     static_cast<const uint32_t*>(nullptr), 0u, b.ngroups, b.gsum, b.lines, b.lines_cap);
-  hipLaunchKernelGGL(k_facc, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.slots, 0u, b.rpk, b.sig_status,
-                     b.pk_status, b.lines, b.lines_cap, b.f, b.ngroups, b.gsum, b.gpair,
-                     static_cast<const bgv_dgroup*>(nullptr), 0u, static_cast<const g1_jac*>(nullptr),
-                     static_cast<fp12_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
-                     static_cast<const uint32_t*>(nullptr));
-  return hipGetLastError();
-}
-
 // The own pairs f_i of the slots of the listed uniform first-pass groups (glist[0, *dcount) <=
 // b.ngroups), for the retry tests; one block per listed group.
 hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,

@@ -95,8 +95,6 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
 // nslots + ngroups exceeds this (else k_final_fold)
 uint32_t bgv_fold_pairs_max();
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
-// retry parts' pairs one per lane through k_lines + k_facc (needs b.lines, lines_cap >= ngroups)
-hipError_t bgv_launch_gpairs_bulk(const bgv_dev_batch& b, hipStream_t st);
 // the own set pairs f_i of the slots of listed uniform first-pass groups (glist[0, *dcount),
 // device memory; bgv_k_miller_bulk.hip; needs the first pass's line records and groups)
 hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,
