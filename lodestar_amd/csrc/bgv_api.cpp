@@ -195,10 +195,6 @@ struct Exec {
   size_t pout_cap = 0;
   uint32_t* d_lines = nullptr;  // the bulk Miller loop's line records (bgv_lines_pairs)
   uint32_t lines_cap = 0;       // pairs
-  // the failing uniform first-pass groups whose slots' own pairs the retry thread computes
-  // (bgv_launch_uniform_refill): [0] their count, [1 + i] group i
-  uint32_t* d_ulist = nullptr;
-  size_t ulist_cap = 0;
 };
 
 // bgv_final_verify's device buffers (under util_mu)
@@ -220,7 +216,7 @@ struct BatchState {
   uint32_t nslots = 0, ngroups = 0;
   std::vector<uint32_t> call_gb;  // each call's first group in the merged batch
   bool want_gu = false;           // the first pass's u values are in x.d_gu1 (pattern tests)
-  std::vector<uint32_t> refill;   // failing uniform groups of shared jobs: their slots' own pairs first
+  bool uniform = false;           // the first pass ran uniform groups (their slots have no own pair f_i)
   bool prof = false;
 };
 // A super-batch whose first pass is done and whose retry rounds wait for the retry thread.
@@ -551,7 +547,19 @@ static int exec_reserve_groups(Exec& x, uint32_t groups) {
 }
 
 // line records for the batch's bulk Miller launch (none on the latency path): allocated on
-// first use, in steps of 16,384 pairs (368 MB), never shrunk
+// first use, in steps of 16,384 pairs (374 MB); kept for the next batch up to the default
+// super-batch's pairs, freed after a larger call (a 2^20-set job alone needs ~24 GB:
+// exec_trim_lines)
+static uint32_t lines_keep_pairs() {
+  const size_t slots = max_batch_slots();
+  return (uint32_t)((slots + slots / BGV_WAVE + 16383u) & ~(size_t)16383u);
+}
+static void exec_trim_lines(Exec& x) {
+  if (x.lines_cap <= lines_keep_pairs()) return;
+  (void)hipFree(x.d_lines);
+  x.d_lines = nullptr;
+  x.lines_cap = 0;
+}
 static int exec_reserve_lines(Exec& x, bgv_dev_batch& b) {
   const uint32_t need = bgv_lines_pairs(b);
   if (need > x.lines_cap) {
@@ -579,7 +587,7 @@ static int exec_create(Exec* x) {
 static void exec_destroy(Exec* x) {
   if (x->main) (void)hipStreamSynchronize(x->main);
   void* ptrs[] = {x->slot_mem, x->group_mem, x->d_slots,    x->d_groups, x->d_idx,
-                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines,  x->d_ulist};
+                  x->d_pkb,      x->d_pscratch, x->d_pout, x->d_lines};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   x->h_slots.release();
@@ -915,7 +923,11 @@ static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int
 // Group testing for one retry round: split every pending unit into parts.  gb: the call's
 // first group in the batch when the first pass's u values are on the device (pattern tests
 // possible), else -1.
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb) {
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb, bool uniform) {
+  // A test inside a uniform first-pass group (whose slots have no own pair f_i) pairs the sum
+  // of its slots' r_i pk_i with the group's one H instead: prod_S e(r_i pk_i, H) =
+  // e(sum_S r_i pk_i, H), the same pairing value, so the complement verdicts hold too
+  auto uflag = [&](uint32_t g) { return uniform && call->L.group_uniform[g] ? BGV_GROUP_UNIFORM : 0u; };
   call->parts.clear();
   call->punits.clear();
   for (size_t ui = 0; ui < call->units.size(); ++ui) {
@@ -949,7 +961,7 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
         pu.tests.push_back((uint32_t)rg.size());
         part.groups.push_back((uint32_t)rg.size());
         part.pattern = (int)call->punits.size();
-        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1), 0});
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1), uflag(ug)});
         call->parts.push_back(std::move(part));
       }
       call->punits.push_back(std::move(pu));
@@ -981,7 +993,7 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
         part.pattern = (int)call->punits.size();
         pu.tests.push_back((uint32_t)rg.size());
         pu.test_jobs.push_back(std::move(tj));
-        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, 0, 0});
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, 0, uflag(ug)});
         call->parts.push_back(std::move(part));
       }
       call->punits.push_back(std::move(pu));
@@ -994,7 +1006,7 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
         Part part;
         part.jobs.push_back(j);
         part.groups.push_back((uint32_t)rg.size());
-        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, job_mask(call, j, g), 0, 0});
+        rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, job_mask(call, j, g), 0, uflag(ug)});
         call->parts.push_back(std::move(part));
       }
       continue;
@@ -1012,10 +1024,13 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
           n += call->jobs[part.jobs[q2]].n_sets;
           ++q2;
         }
-        for (uint32_t off = 0; off < n; off += BGV_WAVE) {
+        // chunks within one first-pass group each (groups start on wave boundaries), so a chunk
+        // of a uniform group takes its flag
+        for (uint32_t off = 0; off < n;) {
+          const uint32_t s0 = first + off, len = std::min<uint32_t>(n - off, BGV_WAVE - s0 % BGV_WAVE);
           part.groups.push_back((uint32_t)rg.size());
-          rg.push_back(
-              bgv_dgroup{call->slot_base + first + off, std::min<uint32_t>(BGV_WAVE, n - off), BGV_ALL_SLOTS, 0, 0});
+          rg.push_back(bgv_dgroup{call->slot_base + s0, len, BGV_ALL_SLOTS, 0, uflag(call->L.slots[s0].group)});
+          off += len;
         }
         q = q2;
       }
@@ -1208,6 +1223,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   bgv_dev_batch b = make_batch(d, x, nslots, ngroups);
   b.max_npk = max_npk;
   b.uniform = uniform;
+  bs.uniform = uniform;
   b.uniq = x.d_idx + nidx;
   b.nuniq = (uint32_t)nuniq;
   if (int lrc = exec_reserve_lines(x, b)) return lrc;
@@ -1238,6 +1254,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   HIPCHK(hipStreamSynchronize(x.main));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+  exec_trim_lines(x);  // the records are dead once the first pass is done
   if (prof) prof_add(c, x, true, true);
   t_pass1 = ms_since(tg);
   const auto tp = std::chrono::steady_clock::now();
@@ -1248,12 +1265,6 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     for (Call* call : calls) {
       call->st.device_ms += ms;
       call_after_pass1(call, ss + call->slot_base, ps + call->slot_base, verdict + gb);
-      // a failing uniform group of shared jobs goes to the retry tests, which multiply its
-      // slots' own pairs: the retry thread computes them first (run_retries)
-      if (uniform)
-        for (size_t gi = 0; gi < call->L.groups.size(); ++gi)
-          if (call->L.group_uniform[gi] && call->L.group_shared[gi] && !(verdict[gb + gi] & 1))
-            bs.refill.push_back(gb + (uint32_t)gi);
       call_gb.push_back(gb);
       gb += (uint32_t)call->L.groups.size();
       for (size_t u = 0; u < call->units.size() && !want_gu; ++u) want_gu = pattern_eligible(call, u);
@@ -1319,21 +1330,6 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
   int rc;
   const auto tr = std::chrono::steady_clock::now();
   int rounds = 0;
-  if (!bs.refill.empty()) {
-    // the failing uniform groups' slots' own pairs, over the first pass's groups, slots, line
-    // records and per-slot results (x still holds them: no round has run yet)
-    const uint32_t nr = (uint32_t)bs.refill.size();
-    std::vector<uint32_t> lst(1 + nr);
-    lst[0] = nr;
-    std::copy(bs.refill.begin(), bs.refill.end(), lst.begin() + 1);
-    if ((rc = grow(&x.d_ulist, &x.ulist_cap, lst.size()))) return rc;
-    HIPCHK(hipMemcpyAsync(x.d_ulist, lst.data(), 4 * lst.size(), hipMemcpyHostToDevice, x.close));
-    b = make_batch(d, x, nslots, bs.ngroups);
-    b.lines = x.d_lines;
-    b.lines_cap = x.lines_cap;
-    HIPCHK(bgv_launch_uniform_refill(b, x.d_ulist + 1, x.d_ulist, x.close));
-    HIPCHK(hipStreamSynchronize(x.close));  // lst leaves scope
-  }
   // retry rounds over the per-slot results on the device
   for (;;) {
     const auto th = std::chrono::steady_clock::now();
@@ -1341,18 +1337,31 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     std::vector<uint32_t> base;
     for (size_t k = 0; k < calls.size(); ++k) {
       base.push_back((uint32_t)rg.size());
-      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1);
+      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1, bs.uniform);
     }
     if (rg.empty()) break;
     ++rounds;
     const uint32_t nrg = (uint32_t)rg.size();
-    if ((rc = exec_reserve_groups(x, nrg))) return rc;
-    HIPCHK(x.h_groups.reserve(nrg));
+    // the tests inside uniform first-pass groups (they pair their pubkey sums, bgv_launch_gpairs),
+    // listed after the groups in the same upload
+    std::vector<uint32_t> upk;
+    if (bs.uniform)
+      for (uint32_t t = 0; t < nrg; ++t)
+        if (rg[t].flags & BGV_GROUP_UNIFORM) upk.push_back(t);
+    const uint32_t per = (uint32_t)(sizeof(bgv_dgroup) / sizeof(uint32_t));
+    const uint32_t nlist = ((uint32_t)upk.size() + per - 1) / per;  // in bgv_dgroup units
+    if ((rc = exec_reserve_groups(x, nrg + nlist))) return rc;
+    HIPCHK(x.h_groups.reserve(nrg + nlist));
     HIPCHK(x.h_verdict.reserve(nrg));
     memcpy(x.h_groups.p, rg.data(), sizeof(bgv_dgroup) * nrg);
+    if (!upk.empty()) memcpy(x.h_groups.p + nrg, upk.data(), 4 * upk.size());
     int32_t* rv = x.h_verdict.p;
-    HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * nrg, hipMemcpyHostToDevice, x.close));
+    HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * (nrg + nlist), hipMemcpyHostToDevice,
+                          x.close));
     b = make_batch(d, x, nslots, nrg);
+    b.uniform = !upk.empty();
+    b.upk = reinterpret_cast<const uint32_t*>(x.d_groups + nrg);
+    b.npk = (uint32_t)upk.size();
     bool pattern = false;
     for (Call* call : calls) pattern = pattern || !call->punits.empty();
     if (pattern) b.gu1 = x.d_gu1;

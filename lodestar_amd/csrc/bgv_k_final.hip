@@ -298,7 +298,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1,
-                       !pairs && b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
+                       b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
   BGV_MARK(5);
   return hipGetLastError();
 }

@@ -55,11 +55,13 @@ __global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ g
 // every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
 // A uniform first-pass group (BGV_GROUP_UNIFORM) also sums its live slots' r_i pk_i into
 // gpk: the group's set pairs are then one pair e(gpk, H) (the same slots k_facc would pair).
-__global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
-                                             const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
-                                             const int32_t* __restrict__ sig_status,
-                                             const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum,
-                                             const g1_jac* __restrict__ rpk, g1_jac* __restrict__ gpk) {
+#define BGV_GSUM_ARGS                                                                                       \
+  const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const bgv_dslot *__restrict__ slots,              \
+      const g2_jac *__restrict__ rsig, const int32_t *__restrict__ sig_status,                               \
+      const int32_t *__restrict__ pk_status, g2_jac *__restrict__ gsum, const g1_jac *__restrict__ rpk,     \
+      g1_jac *__restrict__ gpk
+}  // extern "C"
+__device__ __forceinline__ void gsum_body(BGV_GSUM_ARGS) {
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
@@ -89,16 +91,24 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
   acc = jac_add(acc, point_xor<1>(acc));
   if (gi < ngroups && c == 0) gsum[gi] = acc;
 }
+extern "C" {
+__global__ void __launch_bounds__(64) k_gsum(BGV_GSUM_ARGS) {
+  gsum_body(groups, ngroups, slots, rsig, sig_status, pk_status, gsum, rpk, gpk);
+}
 
 // One Miller loop per team of 16 lanes: pairs [0, nslots) are the sets' e(r pk, H(m)),
 // pairs [nslots, nslots + ngroups) the groups' e(-G1, S_g).  The twist point runs the
 // generated rounds (bgv_tmiller_prog.h) on the team's LDS slots, the Fp12 accumulator is
 // coefficient-parallel.  Teams past the end (and pairs that take no part) compute on
 // zeros and store 1 or nothing, so every lane reaches every barrier.
+// Pairs [nslots + ngroups, + npk) (retry rounds with uniform groups): pair j is test t =
+// upk[j]'s pubkey-sum pair e(gpk_t, H of its root) into gpkp_t (groups[t] is BGV_GROUP_UNIFORM).
 #define BGV_MTEAM_ARGS                                                                                      \
   const bgv_dslot *__restrict__ slots, uint32_t nslots, const g1_jac *__restrict__ rpk,                      \
       const g2_jac *__restrict__ h, const int32_t *__restrict__ sig_status, const int32_t *__restrict__ pk_status, \
-      fp12_t *__restrict__ f, uint32_t ngroups, const g2_jac *__restrict__ gsum, fp12_t *__restrict__ gpair
+      fp12_t *__restrict__ f, uint32_t ngroups, const g2_jac *__restrict__ gsum, fp12_t *__restrict__ gpair,   \
+      const bgv_dgroup *__restrict__ groups, const uint32_t *__restrict__ upk, uint32_t npk,                   \
+      const g1_jac *__restrict__ gpk, fp12_t *__restrict__ gpkp
 }  // extern "C"
 __device__ __forceinline__ void miller_team_body(BGV_MTEAM_ARGS) {
   __shared__ uint8_t prog[TMP_TABLE_BYTES];
@@ -107,18 +117,30 @@ __device__ __forceinline__ void miller_team_body(BGV_MTEAM_ARGS) {
   for (int i = threadIdx.x; i < TMP_TABLE_BYTES; i += 64) prog[i] = kTmProg[i];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
-  const uint32_t total = nslots + ngroups;
+  const uint32_t total = nslots + ngroups + npk;
   const uint32_t u = blockIdx.x * BGV_FINAL_TEAMS + team;
   const uint32_t uu = u < total ? u : total - 1;
-  const bool set_pair = uu < nslots;
+  const bool set_pair = uu < nslots, pk_pair = uu >= nslots + ngroups;
+  const g1_jac* pk_p = nullptr;  // P of a set pair or a pubkey-sum pair
   bool live;
   const fp_t* qsrc;
+  fp12_t* dst;
   if (set_pair) {
     live = slot_live(slots[uu], sig_status[uu], pk_status[uu]);
     qsrc = reinterpret_cast<const fp_t*>(h + slots[uu].hsrc);  // H of the slot's signing root
-  } else {
+    pk_p = rpk + uu;
+    dst = f + uu;
+  } else if (!pk_pair) {
     qsrc = reinterpret_cast<const fp_t*>(gsum + (uu - nslots));
     live = !jac_is_inf(gsum[uu - nslots]);
+    dst = gpair + (uu - nslots);
+  } else {
+    const uint32_t t = upk[uu - nslots - ngroups];
+    const bgv_dgroup G = groups[t];
+    qsrc = reinterpret_cast<const fp_t*>(h + slots[G.first_slot].hsrc);  // the group's one root
+    live = !jac_is_inf(gpk[t]);
+    pk_p = gpk + t;
+    dst = gpkp + t;
   }
   fp_t* Sm = S[team];
   if (c < 6) {
@@ -127,7 +149,7 @@ __device__ __forceinline__ void miller_team_body(BGV_MTEAM_ARGS) {
     Sm[TMP_S_BANK0 + c] = v;
   } else if (c < 9) {
     // P in Jacobian form (bls_pairing.h miller_p): -X Z, Y, Z^3
-    const g1_jac P = set_pair ? rpk[uu] : jac_from_aff(g1_neg_generator());
+    const g1_jac P = pk_p ? *pk_p : jac_from_aff(g1_neg_generator());
     const fp_t v = c == 6 ? fp_neg(fp_mul(P.x, P.z)) : (c == 7 ? P.y : fp_mul(fp_sqr(P.z), P.z));
     Sm[c == 6 ? TMP_S_XN : (c == 7 ? TMP_S_YP : TMP_S_ZP3)] = live ? v : fp_zero();
   } else if (c == 9) {
@@ -173,14 +195,13 @@ __device__ __forceinline__ void miller_team_body(BGV_MTEAM_ARGS) {
     x = o.mul_line(x, l0, l1, l3);
   }
   x = o.conj(x);
-  if (u < total && c < BGV_TEAM_COMPS) {
-    fp12_t* dst = set_pair ? f + uu : gpair + (uu - nslots);
+  if (u < total && c < BGV_TEAM_COMPS && dst)
     reinterpret_cast<fp_t*>(dst)[tm_fp_index(cc)] = live ? x : (cc == 0 ? fp_one() : fp_zero());
-  }
 }
 extern "C" {
 __global__ void __launch_bounds__(64) k_miller_team(BGV_MTEAM_ARGS) {
-  miller_team_body(slots, nslots, rpk, h, sig_status, pk_status, f, ngroups, gsum, gpair);
+  miller_team_body(slots, nslots, rpk, h, sig_status, pk_status, f, ngroups, gsum, gpair, groups, upk, npk, gpk,
+                   gpkp);
 }
 
 // The same pairs with one pair per block for the smallest calls, on two waves that run the
@@ -317,7 +338,9 @@ static void launch_miller_latency(const bgv_dev_batch& b, uint32_t nslots, uint3
                        static_cast<fp12_t*>(nullptr));
   else
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(total, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, nslots, b.rpk,
-                       b.h, b.sig_status, b.pk_status, b.f, ngroups, b.gsum, b.gpair);
+                       b.h, b.sig_status, b.pk_status, b.f, ngroups, b.gsum, b.gpair,
+                       static_cast<const bgv_dgroup*>(nullptr), static_cast<const uint32_t*>(nullptr), 0u,
+                       static_cast<const g1_jac*>(nullptr), static_cast<fp12_t*>(nullptr));
 }
 
 // lanes of one k_miller round: one wave of 64 on each SIMD (MI355X: 256 CUs x 4 SIMDs)
@@ -363,7 +386,9 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
     // the group pairs on extra k_facc lanes would open one more round of one wave per SIMD
     // (131,072 sets + 2,048 groups: 3 rounds instead of 2); run them on teams instead
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, s.main, b.slots, 0u,
-                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair);
+                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair,
+                       static_cast<const bgv_dgroup*>(nullptr), static_cast<const uint32_t*>(nullptr), 0u,
+                       static_cast<const g1_jac*>(nullptr), static_cast<fp12_t*>(nullptr));
     if (bgv_single_pass_miller())
       hipLaunchKernelGGL(k_miller, dim3(nblk(n, 64)), dim3(64), 0, s.main, b.slots, n, b.rpk, b.h, b.sig_status,
                          b.pk_status, b.f, 0u, b.gsum, b.gpair);
@@ -384,12 +409,19 @@ hipError_t bgv_launch_sets(const bgv_dev_batch& b, const bgv_streams& s) {
   return e != hipSuccess ? e : bgv_launch_miller(b, s);
 }
 
-// retry rounds over parts of failed groups: the parts' signature sums and pairs
+// retry rounds over parts of failed groups: the parts' signature sums and pairs; with uniform
+// groups (b.uniform) also the pubkey sums and pubkey-sum pairs of the tests flagged
+// BGV_GROUP_UNIFORM (their slots have no own pair: bgv_api.cpp call_build_parts)
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   if (b.ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
-                     b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk), static_cast<g1_jac*>(nullptr));
-  if (b.ngroups <= bgv_latency_max())
+                     b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk),
+                     b.uniform ? static_cast<g1_jac*>(b.gpk) : static_cast<g1_jac*>(nullptr));
+  if (b.uniform)
+    hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups + b.npk, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u,
+                       b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair, b.groups, b.upk, b.npk,
+                       static_cast<const g1_jac*>(b.gpk), b.gpkp);
+  else if (b.ngroups <= bgv_latency_max())
     launch_miller_latency(b, 0u, b.ngroups, st);
   else
     hipLaunchKernelGGL(k_gpair, dim3(nblk(b.ngroups, 64)), dim3(64), 0, st, b.ngroups, b.gsum, b.gpair);

@@ -83,31 +83,22 @@ __global__ void BGV_KATTR_LINES k_lines(const bgv_dslot* __restrict__ slots, uin
 // an infinite S_g); lanes [nslots + ngroups, nslots + ngroups + npk): a uniform group's
 // (BGV_GROUP_UNIFORM) one set pair MillerLoop(gpk_g, H of its root) into gpkp_g.  The slots of
 // a uniform group take no lane of their own (their f_i stay unwritten: the closing multiplies
-// gpkp instead).  glist (nullable, *dcount first-pass groups: bgv_launch_uniform_refill): block
-// b computes the own pairs f_i of listed group glist[b]'s slots if it is uniform (the retry
-// tests multiply them), and nothing else.
+// gpkp instead; a retry test inside such a group pairs its own pubkey sum, bgv_launch_gpairs).
 __global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint32_t nslots,
                                       const g1_jac* __restrict__ rpk, const int32_t* __restrict__ sig_status,
                                       const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ lines,
                                       uint32_t cap, fp12_t* __restrict__ f, uint32_t ngroups,
                                       const g2_jac* __restrict__ gsum, fp12_t* __restrict__ gpair,
                                       const bgv_dgroup* __restrict__ groups, uint32_t npk,
-                                      const g1_jac* __restrict__ gpk, fp12_t* __restrict__ gpkp,
-                                      const uint32_t* __restrict__ glist, const uint32_t* __restrict__ dcount) {
-  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (glist) {  // refill: the slots of one listed uniform group per block
-    if (blockIdx.x >= *dcount) return;
-    const bgv_dgroup G = groups[glist[blockIdx.x]];
-    if (!(G.flags & BGV_GROUP_UNIFORM) || threadIdx.x >= G.n_slots) return;
-    s = G.first_slot + threadIdx.x;
-  }
+                                      const g1_jac* __restrict__ gpk, fp12_t* __restrict__ gpkp) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   bool live;
   uint32_t lp;
   const g1_jac* P;
   fp12_t* out;
   if (s < nslots) {
     const bgv_dslot& d = slots[s];
-    if (!glist && groups && !(d.flags & BGV_SLOT_PAD) && (groups[d.group].flags & BGV_GROUP_UNIFORM)) return;
+    if (groups && !(d.flags & BGV_SLOT_PAD) && (groups[d.group].flags & BGV_GROUP_UNIFORM)) return;
     live = slot_live(d, sig_status[s], pk_status[s]);
     lp = d.hsrc;
     P = rpk + s;
@@ -186,19 +177,6 @@ hipError_t bgv_launch_miller_bulk(const bgv_dev_batch& b, uint32_t ngroups, hipS
                        ngroups, b.gsum, b.lines, b.lines_cap);
   hipLaunchKernelGGL(k_facc, dim3(nblk(b.nslots + ngroups + npk, 64)), dim3(64), 0, st, b.slots, b.nslots, b.rpk,
                      b.sig_status, b.pk_status, b.lines, b.lines_cap, b.f, ngroups, b.gsum, b.gpair,
-                     b.uniform ? b.groups : nullptr, npk, static_cast<const g1_jac*>(b.gpk), b.gpkp,
-                     static_cast<const uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr));
-  return hipGetLastError();
-}
-
-// The own pairs f_i of the slots of the listed uniform first-pass groups (glist[0, *dcount) <=
-// b.ngroups), for the retry tests; one block per listed group.
-hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,
-                                     hipStream_t st) {
-  if (b.ngroups == 0) return hipSuccess;
-  if (!b.lines) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_facc, dim3(b.ngroups), dim3(64), 0, st, b.slots, b.nslots, b.rpk, b.sig_status, b.pk_status,
-                     b.lines, b.lines_cap, b.f, 0u, b.gsum, b.gpair, b.groups, 0u,
-                     static_cast<const g1_jac*>(b.gpk), b.gpkp, glist, dcount);
+                     b.uniform ? b.groups : nullptr, npk, static_cast<const g1_jac*>(b.gpk), b.gpkp);
   return hipGetLastError();
 }

@@ -52,6 +52,10 @@ struct bgv_dev_batch {
   fp12_t* gpair;       // per group: MillerLoop(-G1, gsum)
   jac_t<fp_t>* gpk;    // per uniform group (BGV_GROUP_UNIFORM): sum of its live r_i pk_i
   fp12_t* gpkp;        // per uniform group: MillerLoop(gpk, H of the group's root)
+  // retry rounds with uniform groups: the npk tests flagged BGV_GROUP_UNIFORM (indices into
+  // groups), whose pubkey-sum pairs bgv_launch_gpairs runs
+  const uint32_t* upk;
+  uint32_t npk;
   fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
   fp12_t* gu;          // per group: u = gprod^((p^2+1) 3 (p^4-p^2+1)/r); pairing value conj(u)/u
   // retry rounds with pattern tests: the first pass's u values (a copy of its gu), indexed by
@@ -95,10 +99,6 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
 // nslots + ngroups exceeds this (else k_final_fold)
 uint32_t bgv_fold_pairs_max();
 hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st);  // retry parts: k_gsum + k_gpair
-// the own set pairs f_i of the slots of listed uniform first-pass groups (glist[0, *dcount),
-// device memory; bgv_k_miller_bulk.hip; needs the first pass's line records and groups)
-hipError_t bgv_launch_uniform_refill(const bgv_dev_batch& b, const uint32_t* glist, const uint32_t* dcount,
-                                     hipStream_t st);
 size_t bgv_slot_bytes();
 size_t bgv_slot_mem_bytes(uint32_t cap_slots);  // the per-slot arrays of an Exec of cap_slots slots
 size_t bgv_group_bytes();

@@ -52,6 +52,6 @@ struct bgv_dgroup {
 // flags: a first-pass group of a bulk batch whose sets all share one signing root (slot
 // first_slot's hsrc) and whose jobs lie inside it.  prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H),
 // so the group's set pairs are ONE Miller loop over its pubkey sum (k_gsum -> gpk, k_facc ->
-// gpkp) and its slots take none; when such a group fails, the retry thread first computes its
-// slots' own pairs for the retry tests (bgv_launch_uniform_refill)
+// gpkp) and its slots take none; a retry test inside such a group (flagged the same,
+// bgv_api.cpp call_build_parts) pairs the sum of its own slots' r_i pk_i the same way
 #define BGV_GROUP_UNIFORM 4u
