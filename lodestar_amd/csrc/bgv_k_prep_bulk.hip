@@ -41,44 +41,6 @@ __global__ void BGV_KATTR_BULK k_prep(const bgv_dslot* __restrict__ slots, uint3
     task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
 }
 
-// k_prep in two phases (BGV_PREP_PHASES=1): k_prep1 runs hash 1, sig 1 and pk, k_prep2 hash 2
-// and sig 2 (bgv_k_tasks.h), the intermediate points in h / rsig
-__global__ void BGV_KATTR_BULK k_prep1(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
-                                       int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
-                                       const uint32_t* __restrict__ pk_idx, const g1_aff* __restrict__ cache,
-                                       const uint8_t* __restrict__ pk_bytes, g1_jac* __restrict__ rpk,
-                                       int32_t* __restrict__ pk_status, const g1_jac* __restrict__ pk_agg,
-                                       const uint32_t* __restrict__ uniq, uint32_t nuniq) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.y == 0) {
-    if (uniq) {
-      if (s < nuniq) task_hash1(uniq[s], slots, h);
-    } else if (s < nslots) {
-      task_hash1(s, slots, h);
-    }
-    return;
-  }
-  if (s >= nslots) return;
-  if (blockIdx.y == 1)
-    task_sig1(s, slots, rsig, sig_status);
-  else
-    task_pk(s, slots, pk_idx, cache, pk_bytes, rpk, pk_status, pk_agg);
-}
-__global__ void BGV_KATTR_BULK k_prep2(const bgv_dslot* __restrict__ slots, uint32_t nslots, g2_jac* __restrict__ rsig,
-                                       const int32_t* __restrict__ sig_status, g2_jac* __restrict__ h,
-                                       const uint32_t* __restrict__ uniq, uint32_t nuniq) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.y == 0) {
-    if (uniq) {
-      if (s < nuniq) task_hash2(uniq[s], slots, h);
-    } else if (s < nslots) {
-      task_hash2(s, slots, h);
-    }
-    return;
-  }
-  if (s < nslots) task_sig2(s, slots, rsig, sig_status);
-}
-
 }  // extern "C"
 
 // BGV_PREP_SPLIT=1 (profiling only: per-task kernel time and counters): the three tasks as
@@ -88,18 +50,6 @@ hipError_t bgv_launch_prep_bulk(const bgv_dev_batch& b, const bgv_streams& s, bo
     const char* e = getenv("BGV_PREP_SPLIT");
     return e && atoi(e) > 0;
   }();
-  static const bool phases = [] {
-    const char* e = getenv("BGV_PREP_PHASES");
-    return e && atoi(e) > 0;
-  }();
-  if (phases) {
-    hipLaunchKernelGGL(k_prep1, dim3(nblk(b.nslots, 64), 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig,
-                       b.sig_status, b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk,
-                       b.pk_status, tree ? b.pk_agg : nullptr, b.uniq, b.nuniq);
-    hipLaunchKernelGGL(k_prep2, dim3(nblk(b.nslots, 64), 2), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig,
-                       b.sig_status, b.h, b.uniq, b.nuniq);
-    return hipGetLastError();
-  }
   for (uint32_t t0 = 0; t0 < 3; t0 += split ? 1 : 3) {
     hipLaunchKernelGGL(k_prep, dim3(nblk(b.nslots, 64), split ? 1 : 3), dim3(64), 0, s.main, b.slots, b.nslots, b.rsig,
                        b.sig_status, b.h, b.pk_idx, reinterpret_cast<const g1_aff*>(b.cache_opaque), b.pk_bytes, b.rpk,

@@ -37,55 +37,6 @@ static __device__ __noinline__ void task_sig(uint32_t s, const bgv_dslot* __rest
   sig_status[s] = st;
 }
 
-// The same two tasks in two phases each (bgv_k_prep_bulk.hip k_prep1 / k_prep2), so that each
-// phase's kernel carries only its own live set: sig 1 decodes and subgroup-checks, leaving the
-// decoded point in rsig[s] (status BGV_ST_OK: the multiplication remains); sig 2 multiplies it
-// by r_i.  hash 1 maps to the curve (h[s] before the cofactor clearing); hash 2 clears it.
-static __device__ __noinline__ void task_sig1(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
-                                              int32_t* __restrict__ sig_status) {
-  const bgv_dslot& d = slots[s];
-  int32_t st = BGV_ST_OK;
-  if (d.flags & BGV_SLOT_PAD) {
-    st = BGV_ST_INFINITY;
-  } else if (d.sig_len != 96) {
-    st = BGV_INVALID_SIZE;
-  } else {
-    uint8_t b[96];
-    for (int i = 0; i < 96; ++i) b[i] = d.sig[i];
-    g2_aff a;
-    bool inf;
-    st = g2_decompress(&a, &inf, b);
-    if (st == BGV_OK) {
-      if (inf) {
-        st = BGV_ST_INFINITY;
-      } else {
-        const g2_jac j = jac_from_aff(a);
-        if (!g2_in_subgroup(j))
-          st = BGV_POINT_NOT_IN_GROUP;
-        else
-          rsig[s] = j;
-      }
-    }
-  }
-  sig_status[s] = st;
-}
-static __device__ __noinline__ void task_sig2(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ rsig,
-                                              const int32_t* __restrict__ sig_status) {
-  if (sig_status[s] != BGV_ST_OK) return;
-  rsig[s] = jac_mul_glv(rsig[s], slots[s].scalar);
-}
-static __device__ __noinline__ void task_hash1(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
-  const bgv_dslot& d = slots[s];
-  if (d.flags & BGV_SLOT_PAD) return;
-  uint8_t msg[32];
-  for (int i = 0; i < 32; ++i) msg[i] = d.msg[i];
-  h[s] = hash_to_curve_g2(msg, 32);
-}
-static __device__ __noinline__ void task_hash2(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
-  if (slots[s].flags & BGV_SLOT_PAD) return;
-  h[s] = g2_clear_cofactor(h[s]);
-}
-
 static __device__ __noinline__ void task_hash(uint32_t s, const bgv_dslot* __restrict__ slots, g2_jac* __restrict__ h) {
   const bgv_dslot& d = slots[s];
   if (d.flags & BGV_SLOT_PAD) return;

@@ -342,18 +342,13 @@ BGV_NOINLINE g2_jac iso_map_g2_jac(const g2_jac& p) {
   return r;
 }
 
-// hash_to_G2 before its cofactor clearing: hash_to_field, both maps (Jacobian), their sum
-BGV_NOINLINE g2_jac hash_to_curve_g2(const uint8_t* msg, uint32_t len) {
+// Full hash_to_G2 of one message: a Jacobian point in G2 (both maps in Jacobian form, no
+// inversion anywhere).
+BGV_NOINLINE g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
   fp2_t u0, u1;
   hash_to_field_fp2(&u0, &u1, msg, len);
   const fp_t sm5 = fp_sqrt_minus5();
   const g2_jac q0 = iso_map_g2_jac(sswu_g2_jac(u0, sm5));
   const g2_jac q1 = iso_map_g2_jac(sswu_g2_jac(u1, sm5));
-  return jac_add(q0, q1);
-}
-
-// Full hash_to_G2 of one message: a Jacobian point in G2 (both maps in Jacobian form, no
-// inversion anywhere).
-BGV_NOINLINE g2_jac hash_to_g2(const uint8_t* msg, uint32_t len) {
-  return g2_clear_cofactor(hash_to_curve_g2(msg, len));
+  return g2_clear_cofactor(jac_add(q0, q1));
 }
