@@ -125,15 +125,6 @@ static bool uniform_enabled() {
 // Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
 // retry rounds of several super-batches then run side by side instead of queueing behind one
 // another (their rounds are latency-bound chains of small launches)
-// BGV_RETRY_ZEROCOPY=1: a retry round's kernels read its groups from and write its verdicts to
-// the page-locked host staging directly (no copy launches in the round's chain), for A/B
-static bool retry_zero_copy() {
-  static const bool v = [] {
-    const char* e = getenv("BGV_RETRY_ZEROCOPY");
-    return e && atoi(e) > 0;
-  }();
-  return v;
-}
 static int retry_threads_per_device() {
   static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
   return v;
@@ -1365,15 +1356,9 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     memcpy(x.h_groups.p, rg.data(), sizeof(bgv_dgroup) * nrg);
     if (!upk.empty()) memcpy(x.h_groups.p + nrg, upk.data(), 4 * upk.size());
     int32_t* rv = x.h_verdict.p;
-    const bool zc = retry_zero_copy();
-    if (!zc)
-      HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * (nrg + nlist), hipMemcpyHostToDevice,
-                            x.close));
+    HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * (nrg + nlist), hipMemcpyHostToDevice,
+                          x.close));
     b = make_batch(d, x, nslots, nrg);
-    if (zc) {  // the kernels read the groups from, and write the verdicts to, page-locked host memory
-      b.groups = x.h_groups.p;
-      b.verdict = rv;
-    }
     b.uniform = !upk.empty();
     b.upk = reinterpret_cast<const uint32_t*>(b.groups + nrg);
     b.npk = (uint32_t)upk.size();
@@ -1385,7 +1370,7 @@ static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls
     HIPCHK(hipEventRecord(x.ev0, x.close));
     HIPCHK(bgv_launch_groups(b, SC, true));
     HIPCHK(hipEventRecord(x.ev1, x.close));
-    if (!zc) HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
+    HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
     HIPCHK(hipStreamSynchronize(x.close));
     const double t_wait = ms_since(tl);
     HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
@@ -1600,14 +1585,11 @@ int bgv_init(const int* devices, int ndev, bgv_ctx** out) {
               hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) == hipSuccess;
     int least = 0, greatest = 0;
     ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
-    // BGV_RETRY_PRIO=0: the retry streams at normal priority (A/B measurements)
-    static const bool retry_high = [] {
-      const char* e = getenv("BGV_RETRY_PRIO");
-      return !(e && atoi(e) == 0);
-    }();
+    // high priority: at normal priority the mainnet-shaped leg measured 2.30-2.73 against
+    // 3.21-3.27 M sets/s (profiles/r05/uniform/mainnet_probe_r05g.jsonl)
     for (int k = 0; ok && k < retry_threads_per_device(); ++k) {
       hipStream_t st = nullptr;
-      ok = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, retry_high ? greatest : least) == hipSuccess;
+      ok = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest) == hipSuccess;
       if (ok) d.sched->retries.push_back(st);
     }
     for (int k = 0; ok && k < dispatchers_per_device(); ++k) {
