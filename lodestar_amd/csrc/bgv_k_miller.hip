@@ -53,15 +53,14 @@ __global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ g
 // S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an
 // infinity signature in the accumulator).  A team of 16 lanes per group: lane c sums
 // every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
-// A uniform first-pass group (BGV_GROUP_UNIFORM) also sums its live slots' r_i pk_i into
-// gpk: the group's set pairs are then one pair e(gpk, H) (the same slots k_facc would pair).
-#define BGV_GSUM_ARGS                                                                                       \
-  const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const bgv_dslot *__restrict__ slots,              \
-      const g2_jac *__restrict__ rsig, const int32_t *__restrict__ sig_status,                               \
-      const int32_t *__restrict__ pk_status, g2_jac *__restrict__ gsum, const g1_jac *__restrict__ rpk,     \
-      g1_jac *__restrict__ gpk
-}  // extern "C"
-__device__ __forceinline__ void gsum_body(BGV_GSUM_ARGS) {
+// A uniform group (BGV_GROUP_UNIFORM: a first-pass group, or a retry test inside one) also sums
+// its live slots' r_i pk_i into gpk: its set pairs are then one pair e(gpk, H) (the same slots
+// k_facc would pair).
+__global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                             const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
+                                             const int32_t* __restrict__ sig_status,
+                                             const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum,
+                                             const g1_jac* __restrict__ rpk, g1_jac* __restrict__ gpk) {
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
@@ -90,10 +89,6 @@ __device__ __forceinline__ void gsum_body(BGV_GSUM_ARGS) {
   acc = jac_add(acc, point_xor<2>(acc));
   acc = jac_add(acc, point_xor<1>(acc));
   if (gi < ngroups && c == 0) gsum[gi] = acc;
-}
-extern "C" {
-__global__ void __launch_bounds__(64) k_gsum(BGV_GSUM_ARGS) {
-  gsum_body(groups, ngroups, slots, rsig, sig_status, pk_status, gsum, rpk, gpk);
 }
 
 // One Miller loop per team of 16 lanes: pairs [0, nslots) are the sets' e(r pk, H(m)),
