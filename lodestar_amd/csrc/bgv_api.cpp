@@ -263,8 +263,9 @@ struct Layout {
   std::vector<std::vector<uint32_t>> job_groups;
   std::vector<uint32_t> job_first_slot;  // first slot of each laid-out job (its slots are contiguous)
   std::vector<char> group_shared;        // group holds sets of more than one job
-  std::vector<char> group_uniform;       // every set of the group shares one signing root and every
-                                         // job in it lies inside it (BGV_GROUP_UNIFORM in bulk batches)
+  std::vector<char> group_uniform;       // every set of the group shares one signing root and no
+                                         // batchable job in it spans groups (BGV_GROUP_UNIFORM in bulk
+                                         // batches)
   std::vector<uint32_t> idx;             // concatenated pubkey indices
   std::vector<uint8_t> pkb;              // concatenated 96-B pubkey records
   std::vector<uint32_t> uniq;            // first slot of each distinct signing root (hash_to_G2 once)
@@ -330,14 +331,19 @@ struct Builder {
     memcpy(s.msg, st.msg, 32);
     if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
     const uint32_t self = (uint32_t)L.slots.size();
-    uint64_t key;
-    memcpy(&key, st.msg, 8);
-    const auto it = first_root.emplace(key, self).first;
-    if (it->second != self && memcmp(L.slots[it->second].msg, st.msg, 32) == 0) {
-      s.hsrc = it->second;  // same root as an earlier slot of this call
+    if (self > 0 && !(L.slots[self - 1].flags & BGV_SLOT_PAD) && memcmp(L.slots[self - 1].msg, st.msg, 32) == 0) {
+      s.hsrc = L.slots[self - 1].hsrc;  // the previous slot's root (committees arrive together)
     } else {
-      s.hsrc = self;
-      L.uniq.push_back(self);
+      uint64_t key;
+      memcpy(&key, st.msg, 8);
+      auto it = first_root.find(key);
+      if (it == first_root.end()) it = first_root.emplace(key, self).first;
+      if (it->second != self && memcmp(L.slots[it->second].msg, st.msg, 32) == 0) {
+        s.hsrc = it->second;  // same root as an earlier slot of this call
+      } else {
+        s.hsrc = self;
+        L.uniq.push_back(self);
+      }
     }
     if (g.n_slots > 0 && L.slots[g.first_slot].hsrc != s.hsrc) L.group_uniform[open_group] = 0;
     L.slots.push_back(s);
@@ -734,6 +740,15 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   Layout& L = call->L;
   L.job_groups.resize(njobs);
   L.job_first_slot.assign(njobs, 0);
+  {
+    size_t npk = 0;
+    for (size_t i = 0; i < nsets; ++i)
+      if (sets[i].pk_indices) npk += sets[i].n_pk;
+    const size_t cap = nsets + nsets / 8 + BGV_WAVE;  // with room for the groups' padding
+    L.slots.reserve(cap);
+    L.slot_set.reserve(cap);
+    L.idx.reserve(npk);
+  }
   Builder B(L);
   for (size_t j = 0; j < njobs; ++j)
     if (call->code[j] == 2) call->todo.push_back(j);
@@ -792,8 +807,12 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
   B.pad_to_wave();
+  // A batchable job over several groups may be retried by fanout over its slots, which needs
+  // their own pairs: its groups are not uniform.  A non-batchable job is never retried (its
+  // verdict is its groups' AND, call_after_pass1), so its groups stay uniform where their sets
+  // share a root: the config-5 sweep's one 2^20-set job, committee by committee.
   for (size_t j : call->todo)
-    if (L.job_groups[j].size() > 1)
+    if (L.job_groups[j].size() > 1 && call->shared_job(j))
       for (uint32_t g : L.job_groups[j]) L.group_uniform[g] = 0;
   call->set_sig.assign(nsets, 0);
   call->set_pk.assign(nsets, 0);
@@ -1183,13 +1202,19 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     size_t ns = 0, ng = 0, ni = 0, npb = 0;
     for (Call* call : calls) {
       const uint32_t ib = (uint32_t)ni, pb = (uint32_t)(npb / 96), gb = (uint32_t)ng;
-      for (bgv_dslot s : call->L.slots) {
-        s.hsrc += call->slot_base;
-        if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
-        if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
-        if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
-        max_npk = std::max(max_npk, s.n_pk);
-        slots[ns++] = s;
+      if (ns == 0 && ib == 0 && pb == 0 && gb == 0) {  // the first call: its layout as it is
+        memcpy(slots, call->L.slots.data(), sizeof(bgv_dslot) * call->L.slots.size());
+        for (const bgv_dslot& s : call->L.slots) max_npk = std::max(max_npk, s.n_pk);
+        ns = call->L.slots.size();
+      } else {
+        for (bgv_dslot s : call->L.slots) {
+          s.hsrc += call->slot_base;
+          if (s.flags & BGV_SLOT_PK_CACHED) s.pk_off += ib;
+          if (s.flags & BGV_SLOT_PK_BYTES) s.pk_off += pb;
+          if (!(s.flags & BGV_SLOT_PAD)) s.group += gb;
+          max_npk = std::max(max_npk, s.n_pk);
+          slots[ns++] = s;
+        }
       }
       for (size_t gi = 0; gi < call->L.groups.size(); ++gi) {
         const bgv_dgroup& g = call->L.groups[gi];
@@ -1312,9 +1337,11 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   bs.prof = prof;
   if (trace_on() && !needs_retry(calls))
     fprintf(stderr,
-            "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
-            "total %.1f ms\n",
-            d.id, calls.size(), nslots, ngroups, t_merge, t_tok, t_sets, t_pass1, t_post, ms_since(tb));
+            "[bgv] dev %d calls %zu slots %u groups %u | submit..dispatch %.1f | merge %.1f tokwait %.1f sets %.1f "
+            "groups %.1f post %.1f total %.1f ms\n",
+            d.id, calls.size(), nslots, ngroups,
+            std::chrono::duration<double, std::milli>(tb - calls.front()->t0).count(), t_merge, t_tok, t_sets,
+            t_pass1, t_post, ms_since(tb));
   return BGV_OK;
 }
 

@@ -50,7 +50,8 @@ struct bgv_dgroup {
 };
 #define BGV_ALL_SLOTS (~0ull)
 // flags: a first-pass group of a bulk batch whose sets all share one signing root (slot
-// first_slot's hsrc) and whose jobs lie inside it.  prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H),
+// first_slot's hsrc) and whose batchable jobs lie inside it (a non-batchable job's groups are
+// never retried).  prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H),
 // so the group's set pairs are ONE Miller loop over its pubkey sum (k_gsum -> gpk, k_facc ->
 // gpkp) and its slots take none; a retry test inside such a group (flagged the same,
 // bgv_api.cpp call_build_parts) pairs the sum of its own slots' r_i pk_i the same way
