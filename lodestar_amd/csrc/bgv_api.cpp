@@ -493,6 +493,22 @@ static uint64_t splitmix64(uint64_t* s) {
 }
 
 // nonzero 64-bit randomizers (blst mul_n_aggregate with 64 random bits)
+// fn(lo, hi) over [0, n) in up to 8 host threads when n is large (a 2^20-set call: the
+// merge's 168 MB of slot records and 8 MB of getrandom output), else inline
+template <class F>
+static void par_ranges(size_t n, F fn) {
+  const size_t kMin = size_t(1) << 17;
+  const unsigned nt = n >= kMin ? std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+  if (nt <= 1) {
+    fn(size_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(fn, n * t / nt, n * (t + 1) / nt);
+  fn(size_t(0), n / nt);
+  for (auto& t : th) t.join();
+}
+
 static void fill_scalars(bgv_ctx* c, uint64_t* out, size_t n) {
   {
     std::lock_guard<std::mutex> lk(c->rng_mu);
@@ -506,13 +522,16 @@ static void fill_scalars(bgv_ctx* c, uint64_t* out, size_t n) {
       return;
     }
   }
-  size_t got = 0;
-  while (got < n * 8) {
-    ssize_t r = getrandom(reinterpret_cast<uint8_t*>(out) + got, n * 8 - got, 0);
-    if (r > 0) got += (size_t)r;
-  }
-  for (size_t i = 0; i < n; ++i)
-    if (out[i] == 0) out[i] = 1;
+  par_ranges(n, [out](size_t lo, size_t hi) {
+    size_t got = 0;
+    uint8_t* p = reinterpret_cast<uint8_t*>(out + lo);
+    while (got < (hi - lo) * 8) {
+      const ssize_t r = getrandom(p + got, (hi - lo) * 8 - got, 0);
+      if (r > 0) got += (size_t)r;
+    }
+    for (size_t i = lo; i < hi; ++i)
+      if (out[i] == 0) out[i] = 1;
+  });
 }
 
 template <class T>
@@ -711,6 +730,85 @@ static int host_job_code(const bgv_ctx* c, const bgv_job& jb, const bgv_set* set
   return BGV_OK;
 }
 
+// The layout Builder makes for a call of ONE non-batchable job of cached-key sets (slots in set
+// order from slot 0, groups of group_slots() consecutive slots, pads to the wave boundary),
+// with the per-slot records filled by several host threads: the config-5 sweep's 2^20-set
+// job took ~50 ms on one thread.  false: not such a call (the Builder lays it out).
+static bool layout_one_job_fast(Call* call, const bgv_job& jb, const bgv_set* sets) {
+  const uint32_t n = jb.n_sets, gs = group_slots();
+  const bgv_set* S = sets + jb.first_set;
+  if (n < (1u << 17)) return false;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!S[i].pk_indices) return false;
+  Layout& L = call->L;
+  // signing roots in order: the previous set's root, else the first set with the same root (a
+  // key collision between different roots opens a root of its own), as Builder::add
+  std::vector<uint32_t> hsrc(n), pk_off(n);
+  std::unordered_map<uint64_t, uint32_t> first_root;
+  uint32_t npk = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    pk_off[i] = npk;
+    npk += S[i].n_pk;
+    if (i > 0 && memcmp(S[i - 1].msg, S[i].msg, 32) == 0) {
+      hsrc[i] = hsrc[i - 1];
+      continue;
+    }
+    uint64_t key;
+    memcpy(&key, S[i].msg, 8);
+    auto it = first_root.find(key);
+    if (it == first_root.end()) it = first_root.emplace(key, i).first;
+    if (it->second != i && memcmp(S[it->second].msg, S[i].msg, 32) == 0) {
+      hsrc[i] = it->second;
+    } else {
+      hsrc[i] = i;
+      L.uniq.push_back(i);
+    }
+  }
+  const uint32_t nslots = (n + BGV_WAVE - 1) / BGV_WAVE * BGV_WAVE, ng = (n + gs - 1) / gs;
+  L.slots.resize(nslots);
+  L.slot_set.resize(nslots);
+  L.idx.resize(npk);
+  par_ranges(nslots, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      bgv_dslot& s = L.slots[i];
+      memset(&s, 0, sizeof(s));
+      if (i >= n) {
+        s.flags = BGV_SLOT_PAD;
+        s.hsrc = (uint32_t)i;
+        L.slot_set[i] = -1;
+        continue;
+      }
+      const bgv_set& st = S[i];
+      s.n_pk = st.n_pk;
+      s.sig_len = st.sig_len;
+      s.group = (uint32_t)(i / gs);
+      s.flags = BGV_SLOT_PK_CACHED;
+      s.pk_off = pk_off[i];
+      memcpy(L.idx.data() + pk_off[i], st.pk_indices, 4ull * st.n_pk);
+      memcpy(s.msg, st.msg, 32);
+      if (st.sig_len == 96) memcpy(s.sig, st.sig, 96);
+      s.hsrc = hsrc[i];
+      L.slot_set[i] = (int32_t)(jb.first_set + i);
+    }
+  });
+  L.groups.resize(ng);
+  L.group_shared.assign(ng, 0);
+  L.group_uniform.assign(ng, 1);
+  for (uint32_t g = 0; g < ng; ++g) {
+    const uint32_t f = g * gs, m = std::min(gs, n - f);
+    L.groups[g] = bgv_dgroup{f, m, BGV_ALL_SLOTS};
+    for (uint32_t k = 1; k < m; ++k)
+      if (hsrc[f + k] != hsrc[f]) {
+        L.group_uniform[g] = 0;
+        break;
+      }
+  }
+  L.job_groups[0].resize(ng);
+  for (uint32_t g = 0; g < ng; ++g) L.job_groups[0][g] = g;
+  L.job_first_slot[0] = 0;
+  return true;
+}
+
 // host-side checks and layout, on the caller's thread
 static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs, const bgv_set* sets, size_t nsets,
                        int mode, int32_t* out, bgv_stats* stats, bgv_done_fn done, void* user, int dev = -1) {
@@ -752,8 +850,10 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   Builder B(L);
   for (size_t j = 0; j < njobs; ++j)
     if (call->code[j] == 2) call->todo.push_back(j);
+  const bool fast = njobs == 1 && call->todo.size() == 1 && !call->shared_job(0) &&
+                    layout_one_job_fast(call, jobs[0], sets);
   for (size_t j : call->todo) {
-    if (call->shared_job(j)) continue;
+    if (call->shared_job(j) || fast) continue;
     B.close_group();
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
@@ -1203,8 +1303,17 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
     for (Call* call : calls) {
       const uint32_t ib = (uint32_t)ni, pb = (uint32_t)(npb / 96), gb = (uint32_t)ng;
       if (ns == 0 && ib == 0 && pb == 0 && gb == 0) {  // the first call: its layout as it is
-        memcpy(slots, call->L.slots.data(), sizeof(bgv_dslot) * call->L.slots.size());
-        for (const bgv_dslot& s : call->L.slots) max_npk = std::max(max_npk, s.n_pk);
+        const bgv_dslot* src = call->L.slots.data();
+        std::atomic<uint32_t> mx{0};
+        par_ranges(call->L.slots.size(), [&](size_t lo, size_t hi) {
+          memcpy(slots + lo, src + lo, sizeof(bgv_dslot) * (hi - lo));
+          uint32_t m = 0;
+          for (size_t i = lo; i < hi; ++i) m = std::max(m, src[i].n_pk);
+          uint32_t cur = mx.load();
+          while (m > cur && !mx.compare_exchange_weak(cur, m)) {
+          }
+        });
+        max_npk = std::max(max_npk, mx.load());
         ns = call->L.slots.size();
       } else {
         for (bgv_dslot s : call->L.slots) {
@@ -1232,7 +1341,9 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   }
   std::vector<uint64_t> sc(nslots);
   fill_scalars(c, sc.data(), nslots);
-  for (uint32_t i = 0; i < nslots; ++i) slots[i].scalar = sc[i];
+  par_ranges(nslots, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) slots[i].scalar = sc[i];
+  });
 
   bool prof;
   {
