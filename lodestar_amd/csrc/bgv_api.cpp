@@ -1494,88 +1494,99 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
 
 // The retry rounds of a super-batch after run_pass1, on x.close (the device's retry stream),
 // over the per-slot results the first pass left in x's buffers.
-static int run_retries(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, BatchState& bs) {
-  const uint32_t nslots = bs.nslots;
-  const std::vector<uint32_t>& call_gb = bs.call_gb;
-  const bool want_gu = bs.want_gu, prof = bs.prof;
-  bgv_streams SC{x.close, prof ? x.kev : nullptr};
-  bgv_dev_batch b;
-  float ms = 0;
-  int rc;
-  const auto tr = std::chrono::steady_clock::now();
+// One super-batch in its retry rounds on a retry thread (retry_loop): the rounds of every batch
+// the thread holds are launched back to back on its stream and waited for together, so a
+// round's launch-to-verdict latency is paid once for all of them.
+struct RetryRun {
+  RetryJob job;
   int rounds = 0;
-  // retry rounds over the per-slot results on the device
-  for (;;) {
-    const auto th = std::chrono::steady_clock::now();
-    std::vector<bgv_dgroup> rg;
-    std::vector<uint32_t> base;
-    for (size_t k = 0; k < calls.size(); ++k) {
-      base.push_back((uint32_t)rg.size());
-      call_build_parts(calls[k], rg, want_gu ? (int64_t)call_gb[k] : -1, bs.uniform);
-    }
-    if (rg.empty()) break;
-    ++rounds;
-    const uint32_t nrg = (uint32_t)rg.size();
-    // the tests inside uniform first-pass groups (they pair their pubkey sums, bgv_launch_gpairs),
-    // listed after the groups in the same upload
-    std::vector<uint32_t> upk;
-    if (bs.uniform)
-      for (uint32_t t = 0; t < nrg; ++t)
-        if (rg[t].flags & BGV_GROUP_UNIFORM) upk.push_back(t);
-    const uint32_t per = (uint32_t)(sizeof(bgv_dgroup) / sizeof(uint32_t));
-    const uint32_t nlist = ((uint32_t)upk.size() + per - 1) / per;  // in bgv_dgroup units
-    if ((rc = exec_reserve_groups(x, nrg + nlist))) return rc;
-    HIPCHK(x.h_groups.reserve(nrg + nlist));
-    HIPCHK(x.h_verdict.reserve(nrg));
-    memcpy(x.h_groups.p, rg.data(), sizeof(bgv_dgroup) * nrg);
-    if (!upk.empty()) memcpy(x.h_groups.p + nrg, upk.data(), 4 * upk.size());
-    int32_t* rv = x.h_verdict.p;
-    HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * (nrg + nlist), hipMemcpyHostToDevice,
-                          x.close));
-    b = make_batch(d, x, nslots, nrg);
-    b.uniform = !upk.empty();
-    b.upk = reinterpret_cast<const uint32_t*>(b.groups + nrg);
-    b.npk = (uint32_t)upk.size();
-    bool pattern = false;
-    for (Call* call : calls) pattern = pattern || !call->punits.empty();
-    if (pattern) b.gu1 = x.d_gu1;
-    const double t_build = ms_since(th);
-    const auto tl = std::chrono::steady_clock::now();
-    HIPCHK(hipEventRecord(x.ev0, x.close));
-    HIPCHK(bgv_launch_groups(b, SC, true));
-    HIPCHK(hipEventRecord(x.ev1, x.close));
-    HIPCHK(hipMemcpyAsync(rv, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
-    HIPCHK(hipStreamSynchronize(x.close));
-    const double t_wait = ms_since(tl);
-    HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
-    if (prof) prof_add(c, x, false, true);
-    if (trace_on()) {
-      size_t npt = 0;
-      for (Call* call : calls)
-        for (const PatternUnit& pu : call->punits) npt += pu.tests.size();
-      fprintf(stderr,
-              "[bgv]  round %d: %u groups (%zu tests with a reference), host %.2f, launch..verdicts %.2f, device %.2f ms, "
-              "since round start %.1f ms\n",
-              rounds, nrg, npt, t_build, t_wait, ms, ms_since(tr));
-    }
-    for (size_t k = 0; k < calls.size(); ++k) {
-      Call* call = calls[k];
-      call->st.device_ms += ms;
-      uint32_t mine = 0;
-      for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
-      call->st.device_groups += mine;
-      // part group indices are global to this round
-      call_after_round(call, rv);
-    }
-  }
-  const double t_retry = ms_since(tr);
-  if (trace_on())
-    fprintf(stderr,
-            "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
-            "retry(%d) %.1f total %.1f ms\n",
-            d.id, calls.size(), nslots, bs.ngroups, bs.t_merge, bs.t_tok, bs.t_sets, bs.t_pass1, bs.t_post, rounds,
-            t_retry, ms_since(bs.tb));
+  uint32_t nrg = 0;  // groups of the round in flight (0: none)
+  double t_build = 0;
+  std::chrono::steady_clock::time_point tr;
+};
+
+// Builds r's next round and enqueues it on its Exec's retry stream (groups up, kernels,
+// verdicts down).  *more = false: the batch has no parts left (its rounds are done).
+static int retry_launch(Device& d, RetryRun& r, bool* more) {
+  Exec& x = *r.job.x;
+  std::vector<Call*>& calls = r.job.calls;
+  BatchState& bs = *r.job.st;
+  const auto th = std::chrono::steady_clock::now();
+  std::vector<bgv_dgroup> rg;
+  for (size_t k = 0; k < calls.size(); ++k)
+    call_build_parts(calls[k], rg, bs.want_gu ? (int64_t)bs.call_gb[k] : -1, bs.uniform);
+  *more = !rg.empty();
+  r.nrg = 0;
+  if (rg.empty()) return BGV_OK;
+  ++r.rounds;
+  const uint32_t nrg = (uint32_t)rg.size();
+  // the tests inside uniform first-pass groups (they pair their pubkey sums, bgv_launch_gpairs),
+  // listed after the groups in the same upload
+  std::vector<uint32_t> upk;
+  if (bs.uniform)
+    for (uint32_t t = 0; t < nrg; ++t)
+      if (rg[t].flags & BGV_GROUP_UNIFORM) upk.push_back(t);
+  const uint32_t per = (uint32_t)(sizeof(bgv_dgroup) / sizeof(uint32_t));
+  const uint32_t nlist = ((uint32_t)upk.size() + per - 1) / per;  // in bgv_dgroup units
+  int rc;
+  if ((rc = exec_reserve_groups(x, nrg + nlist))) return rc;
+  HIPCHK(x.h_groups.reserve(nrg + nlist));
+  HIPCHK(x.h_verdict.reserve(nrg));
+  memcpy(x.h_groups.p, rg.data(), sizeof(bgv_dgroup) * nrg);
+  if (!upk.empty()) memcpy(x.h_groups.p + nrg, upk.data(), 4 * upk.size());
+  HIPCHK(hipMemcpyAsync(x.d_groups, x.h_groups.p, sizeof(bgv_dgroup) * (nrg + nlist), hipMemcpyHostToDevice,
+                        x.close));
+  bgv_dev_batch b = make_batch(d, x, bs.nslots, nrg);
+  b.uniform = !upk.empty();
+  b.upk = reinterpret_cast<const uint32_t*>(b.groups + nrg);
+  b.npk = (uint32_t)upk.size();
+  bool pattern = false;
+  for (Call* call : calls) pattern = pattern || !call->punits.empty();
+  if (pattern) b.gu1 = x.d_gu1;
+  r.t_build = ms_since(th);
+  bgv_streams SC{x.close, bs.prof ? x.kev : nullptr};
+  HIPCHK(hipEventRecord(x.ev0, x.close));
+  HIPCHK(bgv_launch_groups(b, SC, true));
+  HIPCHK(hipEventRecord(x.ev1, x.close));
+  HIPCHK(hipMemcpyAsync(x.h_verdict.p, b.verdict, 4ull * nrg, hipMemcpyDeviceToHost, x.close));
+  r.nrg = nrg;
   return BGV_OK;
+}
+
+// After the stream has drained: the round's verdicts into r's calls
+static int retry_complete(bgv_ctx* c, RetryRun& r, double t_wait) {
+  Exec& x = *r.job.x;
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+  if (r.job.st->prof) prof_add(c, x, false, true);
+  if (trace_on()) {
+    size_t npt = 0;
+    for (Call* call : r.job.calls)
+      for (const PatternUnit& pu : call->punits) npt += pu.tests.size();
+    fprintf(stderr,
+            "[bgv]  round %d: %u groups (%zu tests with a reference), host %.2f, launch..verdicts %.2f, device %.2f ms, "
+            "since round start %.1f ms\n",
+            r.rounds, r.nrg, npt, r.t_build, t_wait, ms, ms_since(r.tr));
+  }
+  for (Call* call : r.job.calls) {
+    call->st.device_ms += ms;
+    uint32_t mine = 0;
+    for (const Part& p : call->parts) mine += (uint32_t)p.groups.size();
+    call->st.device_groups += mine;
+    call_after_round(call, x.h_verdict.p);  // part group indices are global to this round
+  }
+  r.nrg = 0;
+  return BGV_OK;
+}
+
+static void retry_trace_done(const Device& d, const RetryRun& r) {
+  if (!trace_on()) return;
+  const BatchState& bs = *r.job.st;
+  fprintf(stderr,
+          "[bgv] dev %d calls %zu slots %u groups %u | merge %.1f tokwait %.1f sets %.1f groups %.1f post %.1f "
+          "retry(%d) %.1f total %.1f ms\n",
+          d.id, r.job.calls.size(), bs.nslots, bs.ngroups, bs.t_merge, bs.t_tok, bs.t_sets, bs.t_pass1, bs.t_post,
+          r.rounds, ms_since(r.tr), ms_since(bs.tb));
 }
 
 static Exec* exec_acquire(Device& d) {
@@ -1609,28 +1620,67 @@ static void finish_calls(std::vector<Call*>& calls, int rc) {
 
 // The device's retry thread: the retry rounds of handed-over super-batches, in order; drains
 // the queue before it stops.
+// The retry thread holds every batch handed over so far and runs their rounds side by side: each
+// pass launches one round of every held batch on the thread's stream, waits once, and applies
+// the verdicts; a batch joins at the next pass after its hand-over and leaves (its calls
+// finished, its Exec released) when it has no parts left.  Under load, when hand-overs queue up,
+// several batches share each launch-to-verdict wait instead of taking turns.
 static void retry_loop(bgv_ctx* c, Device* d, int k) {
   DevSched& s = *d->sched;
   (void)hipSetDevice(d->id);
+  hipStream_t st = s.retries[k];
+  std::vector<RetryRun> held;
+  auto leave = [&](size_t i, int rc) {
+    finish_calls(held[i].job.calls, rc);
+    exec_release(*d, held[i].job.x);
+    c->running.fetch_sub(1);
+    held.erase(held.begin() + (std::ptrdiff_t)i);
+  };
   for (;;) {
-    RetryJob job;
     {
       std::unique_lock<std::mutex> lk(s.mu);
-      s.cv.wait(lk, [&s] { return s.stop || !s.rq.empty(); });
-      if (s.rq.empty()) return;
-      job = std::move(s.rq.front());
-      s.rq.pop_front();
+      if (held.empty()) s.cv.wait(lk, [&s] { return s.stop || !s.rq.empty(); });
+      if (held.empty() && s.rq.empty()) return;  // stopping, and the queue is drained
+      while (!s.rq.empty()) {
+        RetryRun r;
+        r.job = std::move(s.rq.front());
+        s.rq.pop_front();
+        r.job.x->close = st;
+        r.tr = std::chrono::steady_clock::now();
+        // No cache_mu here: the retry kernels (k_gsum, the group pairs, the closing) read only
+        // the per-slot results of pass 1 (r_i sig_i, r_i pk_i, f_i, H, u values), never the
+        // pubkey cache, and bgv_close joins this thread before it frees the devices.  A batch in
+        // its retry rounds keeps the device busy, so it counts as running for the coalescing
+        // window.
+        c->running.fetch_add(1);
+        held.push_back(std::move(r));
+      }
     }
-    job.x->close = s.retries[k];
-    // No cache_mu here: the retry kernels (k_gsum, the group pairs, the closing) read only the
-    // per-slot results of pass 1 (r_i sig_i, f_i, u values), never the pubkey cache, and
-    // bgv_close joins this thread before it frees the devices.  A batch in its retry rounds
-    // keeps the device busy, so it counts as running for the coalescing window.
-    c->running.fetch_add(1);
-    const int rc = run_retries(c, *d, *job.x, job.calls, *job.st);
-    c->running.fetch_sub(1);
-    finish_calls(job.calls, rc);
-    exec_release(*d, job.x);
+    (void)hipSetDevice(d->id);
+    for (size_t i = 0; i < held.size();) {
+      bool more = false;
+      const int rc = retry_launch(*d, held[i], &more);
+      if (rc != BGV_OK) {  // a device error fails this batch's calls; the others go on
+        (void)hipStreamSynchronize(st);
+        leave(i, rc);
+      } else if (!more) {
+        retry_trace_done(*d, held[i]);
+        leave(i, BGV_OK);
+      } else {
+        ++i;
+      }
+    }
+    if (held.empty()) continue;
+    const auto tl = std::chrono::steady_clock::now();
+    const hipError_t e = hipStreamSynchronize(st);
+    const double t_wait = ms_since(tl);
+    for (size_t i = 0; i < held.size();) {
+      const int rc = e == hipSuccess ? retry_complete(c, held[i], t_wait) : -BGV_E_DEVICE;
+      if (rc != BGV_OK)
+        leave(i, rc);
+      else
+        ++i;
+    }
   }
 }
 
