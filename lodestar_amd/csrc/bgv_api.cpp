@@ -120,6 +120,15 @@ static bool uniform_enabled() {
   }();
   return v;
 }
+// BGV_WEIGHTED_UNIFORM=0: failing uniform groups take the pattern tests at once (no weighted
+// test first; call_build_parts), for A/B measurements
+static bool weighted_uniform_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("BGV_WEIGHTED_UNIFORM");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
 // calls with fewer batchable one-set jobs take the latency path: their jobs keep their order
 #define BGV_UNIFORM_MIN_JOBS 1024
 
@@ -405,7 +414,7 @@ struct Part {  // one retry test: consecutive jobs of one failing unit, and the 
 // a failing pair next to other failures are tested alone in one more round.
 struct PatternUnit {
   uint32_t group = 0;              // the call's first-pass group
-  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs
+  int kind = 0;                    // 0: pattern tests S_j; 1: pairs and single jobs; 2: one weighted test
   std::vector<size_t> jobs;        // kind 0: its jobs in slot order
   std::vector<uint32_t> tests;     // round group index of each test
   std::vector<std::vector<size_t>> test_jobs;  // kind 1: each test's jobs
@@ -1089,7 +1098,36 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
     const auto& u = call->units[ui];
     const int ug = call->unit_group[ui], urounds = call->unit_rounds[ui];
     const bool in_group = unit_in_group(call, u, ug);
-    const bool eligible = gb >= 0 && in_group && urounds == 0 && u.size() >= 2 && pattern_eligible(call, ui);
+    const bool eligible = gb >= 0 && in_group && urounds <= 0 && u.size() >= 2 && pattern_eligible(call, ui);
+    if (eligible && urounds == 0 && uflag((uint32_t)ug) && weighted_uniform_enabled()) {
+      // a failing uniform group almost always holds ONE invalid slot (a wrong key): one test with
+      // slot k weighted by k + 1 names it (BGV_GROUP_WEIGHTED; k_final12 finds w with V^w = W)
+      // instead of ~6 pattern tests of two Miller loops each; otherwise the pattern tests follow
+      // (unit_rounds -1).  Two or more invalid slots match some w <= 64 only with negligible
+      // probability (their values are independent elements of prime order r).
+      PatternUnit pu;
+      pu.group = (uint32_t)ug;
+      pu.kind = 2;
+      const bgv_dgroup& g = call->L.groups[pu.group];
+      std::vector<std::pair<uint32_t, size_t>> order;
+      for (size_t j : u) order.emplace_back(call->L.job_first_slot[j], j);
+      std::sort(order.begin(), order.end());
+      uint64_t m = 0;
+      for (const auto& o : order) {
+        pu.jobs.push_back(o.second);
+        m |= job_mask(call, o.second, g);
+      }
+      Part part;
+      part.jobs = pu.jobs;
+      part.groups.push_back((uint32_t)rg.size());
+      part.pattern = (int)call->punits.size();
+      pu.tests.push_back((uint32_t)rg.size());
+      rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1),
+                              BGV_GROUP_UNIFORM | BGV_GROUP_WEIGHTED});
+      call->parts.push_back(std::move(part));
+      call->punits.push_back(std::move(pu));
+      continue;
+    }
     if (eligible) {
       PatternUnit pu;
       pu.group = (uint32_t)ug;
@@ -1222,6 +1260,25 @@ static void call_after_round(Call* call, const int32_t* rv) {
     }
   }
   for (const PatternUnit& pu : call->punits) {
+    if (pu.kind == 2) {  // one weighted test: bits 8..15 = w, slot w - 1 the lone invalid one
+      const int32_t v = rv[pu.tests[0]];
+      const uint32_t w = ((uint32_t)v >> 8) & 0xffu;
+      const bgv_dgroup& g = call->L.groups[pu.group];
+      size_t bad = SIZE_MAX;
+      if (w >= 1 && w <= g.n_slots)
+        for (size_t j : pu.jobs)
+          if ((job_mask(call, j, g) >> (w - 1)) & 1) bad = j;
+      if (bad != SIZE_MAX) {
+        for (size_t j : pu.jobs) call->code[j] = j == bad ? 0 : 1;
+      } else {  // not a lone invalid slot: the pattern tests next round
+        call->units.push_back(pu.jobs);
+        call->unit_group.push_back((int)pu.group);
+        call->unit_rounds.push_back(-1);
+        call->unit_idx.emplace_back();
+        call->unit_dmask.push_back(0);
+      }
+      continue;
+    }
     if (pu.kind == 1) {  // pairs and single jobs (see PatternUnit)
       std::vector<size_t> failing;
       for (size_t t = 0; t < pu.tests.size(); ++t)

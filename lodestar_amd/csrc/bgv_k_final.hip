@@ -118,7 +118,26 @@ __device__ __forceinline__ void final12_body(BGV_FINAL12_ARGS) {
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  const int32_t v = verdict_bits(o, u, g, gu1, fi);
+  int32_t v = verdict_bits(o, u, g, gu1, fi);
+  // weighted tests (BGV_GROUP_WEIGHTED, retry rounds with gu1): the first w with V^w = W, V the
+  // value of group ref1 - 1 and W this one (values conj(u) / u: u_ref^w conj(u) in Fp6); every
+  // team of the block runs the loop when one needs it (the barriers inside o.mul)
+  const bool wt = gu1 && live && (g.flags & BGV_GROUP_WEIGHTED) && g.ref1;
+  if (c == 0) lens[team] = wt ? g.n_slots : 0u;
+  if (__syncthreads_or(wt ? 1 : 0)) {
+    uint32_t wmax = 0;
+    BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) wmax = lens[t] > wmax ? lens[t] : wmax;
+    const fp_t ur = wt ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : one_c;
+    const fp_t cu = o.conj(u);
+    fp_t P = ur;
+    int32_t found = 0;
+    BGV_NO_UNROLL for (uint32_t w = 1; w <= wmax; ++w) {
+      const bool hit = o.is_fp6(o.mul(P, cu));
+      if (wt && hit && found == 0 && w <= g.n_slots) found = (int32_t)w;
+      P = o.mul(P, ur);
+    }
+    if (wt) v = (v & 1) | (found << 8);
+  }
   if (live && c == 0) verdict[gi] = v;
 }
 extern "C" {

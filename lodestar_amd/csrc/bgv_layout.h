@@ -56,3 +56,8 @@ struct bgv_dgroup {
 // gpkp) and its slots take none; a retry test inside such a group (flagged the same,
 // bgv_api.cpp call_build_parts) pairs the sum of its own slots' r_i pk_i the same way
 #define BGV_GROUP_UNIFORM 4u
+// flags: a retry test over a whole failing uniform group with slot k weighted by k + 1
+// (bgv_api.cpp PatternUnit kind 2): k_gsum forms sum (k+1) r_k sig_k and sum (k+1) r_k pk_k,
+// and k_final12 reports in verdict bits 8..15 the w <= n_slots with V^w = W against the
+// first-pass value V of group ref1 - 1 (0: none) -- the slot w - 1 when exactly one is invalid
+#define BGV_GROUP_WEIGHTED 8u
