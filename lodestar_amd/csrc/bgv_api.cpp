@@ -1597,6 +1597,7 @@ static int retry_launch(Device& d, RetryRun& r, bool* more) {
   b.uniform = !upk.empty();
   b.upk = reinterpret_cast<const uint32_t*>(b.groups + nrg);
   b.npk = (uint32_t)upk.size();
+  for (const bgv_dgroup& t : rg) b.weighted = b.weighted || (t.flags & BGV_GROUP_WEIGHTED);
   bool pattern = false;
   for (Call* call : calls) pattern = pattern || !call->punits.empty();
   if (pattern) b.gu1 = x.d_gu1;

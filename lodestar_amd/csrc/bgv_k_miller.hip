@@ -85,7 +85,47 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
-  if (g.flags & BGV_GROUP_WEIGHTED) {  // a whole uniform group, slot k weighted by k + 1 (uniform over the team)
+  if (g.flags & BGV_GROUP_WEIGHTED) return;  // k_gsum_w's (uniform over the team)
+  g2_jac acc = jac_infinity<fp2_t>();
+  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+    if (!grp_has(g, k)) continue;
+    const uint32_t s = g.first_slot + k;
+    const int32_t ss = sig_status[s];
+    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
+  }
+  if (gpk && (g.flags & BGV_GROUP_UNIFORM)) {  // uniform over the team
+    g1_jac pa = jac_infinity<fp_t>();
+    for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
+      if (!grp_has(g, k)) continue;
+      const uint32_t s = g.first_slot + k;
+      if (slot_live(slots[s], sig_status[s], pk_status[s])) pa = jac_add(pa, rpk[s]);
+    }
+    pa = jac_add(pa, point_xor<8>(pa));
+    pa = jac_add(pa, point_xor<4>(pa));
+    pa = jac_add(pa, point_xor<2>(pa));
+    pa = jac_add(pa, point_xor<1>(pa));
+    if (gi < ngroups && c == 0) gpk[gi] = pa;
+  }
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (gi < ngroups && c == 0) gsum[gi] = acc;
+}
+
+// The weighted tests' sums (BGV_GROUP_WEIGHTED: a whole uniform group, slot k weighted by k + 1):
+// sum (k + 1) r_k sig_k into gsum and sum (k + 1) r_k pk_k into gpk, one team of 16 lanes per
+// group as k_gsum.  A kernel of its own: its point arrays would give k_gsum a 7 KB stack frame.
+__global__ void __launch_bounds__(64) k_gsum_w(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                               const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
+                                               const int32_t* __restrict__ sig_status,
+                                               const int32_t* __restrict__ pk_status, g2_jac* __restrict__ gsum,
+                                               const g1_jac* __restrict__ rpk, g1_jac* __restrict__ gpk) {
+  const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
+  const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
+  if (!(g.flags & BGV_GROUP_WEIGHTED)) return;  // k_gsum's (uniform over the team)
+  {
     g2_jac ps[4];
     g1_jac pk[4];
     BGV_UNROLL for (int t = 0; t < 4; ++t) {
@@ -116,31 +156,6 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
     }
     return;
   }
-  g2_jac acc = jac_infinity<fp2_t>();
-  for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
-    if (!grp_has(g, k)) continue;
-    const uint32_t s = g.first_slot + k;
-    const int32_t ss = sig_status[s];
-    if (ss == BGV_ST_OK && slot_live(slots[s], ss, pk_status[s])) acc = jac_add(acc, rsig[s]);
-  }
-  if (gpk && (g.flags & BGV_GROUP_UNIFORM)) {  // uniform over the team
-    g1_jac pa = jac_infinity<fp_t>();
-    for (uint32_t k = (uint32_t)c; k < g.n_slots; k += BGV_TEAM) {
-      if (!grp_has(g, k)) continue;
-      const uint32_t s = g.first_slot + k;
-      if (slot_live(slots[s], sig_status[s], pk_status[s])) pa = jac_add(pa, rpk[s]);
-    }
-    pa = jac_add(pa, point_xor<8>(pa));
-    pa = jac_add(pa, point_xor<4>(pa));
-    pa = jac_add(pa, point_xor<2>(pa));
-    pa = jac_add(pa, point_xor<1>(pa));
-    if (gi < ngroups && c == 0) gpk[gi] = pa;
-  }
-  acc = jac_add(acc, point_xor<8>(acc));
-  acc = jac_add(acc, point_xor<4>(acc));
-  acc = jac_add(acc, point_xor<2>(acc));
-  acc = jac_add(acc, point_xor<1>(acc));
-  if (gi < ngroups && c == 0) gsum[gi] = acc;
 }
 
 // One Miller loop per team of 16 lanes: pairs [0, nslots) are the sets' e(r pk, H(m)),
@@ -474,6 +489,10 @@ hipError_t bgv_launch_gpairs(const bgv_dev_batch& b, hipStream_t st) {
   hipLaunchKernelGGL(k_gsum, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups, b.slots,
                      b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk),
                      b.uniform ? static_cast<g1_jac*>(b.gpk) : static_cast<g1_jac*>(nullptr));
+  if (b.weighted)
+    hipLaunchKernelGGL(k_gsum_w, dim3(nblk(b.ngroups, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.groups, b.ngroups,
+                       b.slots, b.rsig, b.sig_status, b.pk_status, b.gsum, static_cast<const g1_jac*>(b.rpk),
+                       static_cast<g1_jac*>(b.gpk));
   if (b.uniform)
     hipLaunchKernelGGL(k_miller_team, dim3(nblk(b.ngroups + b.npk, BGV_FINAL_TEAMS)), dim3(64), 0, st, b.slots, 0u,
                        b.rpk, b.h, b.sig_status, b.pk_status, b.f, b.ngroups, b.gsum, b.gpair, b.groups, b.upk, b.npk,

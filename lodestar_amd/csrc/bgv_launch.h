@@ -56,6 +56,7 @@ struct bgv_dev_batch {
   // groups), whose pubkey-sum pairs bgv_launch_gpairs runs
   const uint32_t* upk;
   uint32_t npk;
+  bool weighted;  // some of the round's tests are BGV_GROUP_WEIGHTED (k_gsum_w)
   fp12_t* gprod;       // per group: its Miller-loop product (before the final exponentiation)
   fp12_t* gu;          // per group: u = gprod^((p^2+1) 3 (p^4-p^2+1)/r); pairing value conj(u)/u
   // retry rounds with pattern tests: the first pass's u values (a copy of its gu), indexed by
