@@ -118,27 +118,42 @@ __device__ __forceinline__ void final12_body(BGV_FINAL12_ARGS) {
   if (gprod && live) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   const fp_t u = tm_final_exp_u(o, x);
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
-  int32_t v = verdict_bits(o, u, g, gu1, fi);
-  // weighted tests (BGV_GROUP_WEIGHTED, retry rounds with gu1): the first w with V^w = W, V the
-  // value of group ref1 - 1 and W this one (values conj(u) / u: u_ref^w conj(u) in Fp6); every
-  // team of the block runs the loop when one needs it (the barriers inside o.mul)
-  const bool wt = gu1 && live && (g.flags & BGV_GROUP_WEIGHTED) && g.ref1;
-  if (c == 0) lens[team] = wt ? g.n_slots : 0u;
-  if (__syncthreads_or(wt ? 1 : 0)) {
-    uint32_t wmax = 0;
-    BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) wmax = lens[t] > wmax ? lens[t] : wmax;
-    const fp_t ur = wt ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : one_c;
-    const fp_t cu = o.conj(u);
-    fp_t P = ur;
-    int32_t found = 0;
-    BGV_NO_UNROLL for (uint32_t w = 1; w <= wmax; ++w) {
-      const bool hit = o.is_fp6(o.mul(P, cu));
-      if (wt && hit && found == 0 && w <= g.n_slots) found = (int32_t)w;
-      P = o.mul(P, ur);
-    }
-    if (wt) v = (v & 1) | (found << 8);
-  }
+  const int32_t v = verdict_bits(o, u, g, gu1, fi);
   if (live && c == 0) verdict[gi] = v;
+}
+
+// Weighted tests (BGV_GROUP_WEIGHTED) after k_final12 of a retry round: the first w <= n_slots
+// with V^w = W, V the value of first-pass group ref1 - 1 and W the test's (values conj(u) / u:
+// u_ref^w conj(u) in Fp6), into verdict bits 8..15 (0: none).  Teams of 12 lanes as k_final12;
+// every team of a block runs to the block's longest group (the barriers inside o.mul).
+extern "C" __global__ void __launch_bounds__(64) k_final_wident(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
+                                                     const fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
+                                                     int32_t* __restrict__ verdict) {
+  __shared__ fp_t lds[BGV_FINAL12_TEAMS + 1][2 * BGV_TEAM_COMPS];
+  __shared__ uint32_t lens[BGV_FINAL12_TEAMS + 1];
+  const int team = threadIdx.x / BGV_TEAM_COMPS, c = threadIdx.x % BGV_TEAM_COMPS;
+  const uint32_t gi = blockIdx.x * BGV_FINAL12_TEAMS + team;
+  const bool live = team < BGV_FINAL12_TEAMS && gi < ngroups;
+  const bgv_dgroup g = groups[live ? gi : ngroups - 1];
+  const bool wt = live && (g.flags & BGV_GROUP_WEIGHTED) && g.ref1;
+  if (c == 0) lens[team] = wt ? g.n_slots : 0u;
+  if (!__syncthreads_or(wt ? 1 : 0)) return;  // the whole block: no weighted test
+  uint32_t wmax = 0;
+  BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) wmax = lens[t] > wmax ? lens[t] : wmax;
+  const int fi = tm_fp_index(c);
+  const fp_t one_c = c == 0 ? fp_one() : fp_zero();
+  tm_dev_ops_t<BGV_TEAM_COMPS> o{lds[team], lds[team] + BGV_TEAM_COMPS, c, c};
+  const fp_t u = wt ? reinterpret_cast<const fp_t*>(gu + gi)[fi] : one_c;
+  const fp_t ur = wt ? reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[fi] : one_c;
+  const fp_t cu = o.conj(u);
+  fp_t P = ur;
+  int32_t found = 0;
+  BGV_NO_UNROLL for (uint32_t w = 1; w <= wmax; ++w) {
+    const bool hit = o.is_fp6(o.mul(P, cu));
+    if (wt && hit && found == 0 && w <= g.n_slots) found = (int32_t)w;
+    P = o.mul(P, ur);
+  }
+  if (wt && c == 0) verdict[gi] = (verdict[gi] & 1) | (found << 8);
 }
 extern "C" {
 // Two waves per SIMD: the same 250 VGPRs and 128 B of scratch per lane as at one, and the teams'
@@ -309,6 +324,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     const char* e = getenv("BGV_FOLD_LEAN");
     return !(e && atoi(e) == 0);
   }();
+  if (b.weighted && !b.gu) return hipErrorInvalidValue;
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
@@ -318,6 +334,9 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1,
                        b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
+  if (b.weighted)
+    hipLaunchKernelGGL(k_final_wident, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
+                       b.ngroups, static_cast<const fp12_t*>(b.gu), b.gu1, b.verdict);
   BGV_MARK(5);
   return hipGetLastError();
 }
