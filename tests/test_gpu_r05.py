@@ -176,3 +176,32 @@ def test_uniform_groups_one_job(ctxs):
     bad[5000] = native.SetSpec(roots[5000], sets[5000].sig, pk_indices=[(5000 + 1) % NKEYS])
     for c in (one, two):
         assert c.verify_jobs([(bad, False)], native.MODE_WORKER) == [0]
+
+
+def test_uniform_groups_weighted_positions(ctxs):
+    """The weighted test of a failing uniform group (BGV_GROUP_WEIGHTED: slot k weighted by k + 1,
+    the lone invalid slot named as the w with V^w = W): wrong keys at the first slot of one group
+    and the last slot of another (w = 1 and w = 64), one beside an undecodable signature (a dead
+    slot, its weight skipped), and two in one group (no w matches: the pattern tests follow).
+    Every verdict equals the job verified alone."""
+    from lodestar_amd import native
+    (one, _), sks = ctxs
+    n = 24576
+    committee = 256  # four aligned 64-set groups per root
+    roots = [hashlib.sha256(b"r05-weighted-%d" % (i // committee)).digest() for i in range(n)]
+    keys = [(i * 11) % NKEYS for i in range(n)]
+    sigs = one.sign(b"".join(sks[k] for k in keys), b"".join(roots))
+    sets = [native.SetSpec(roots[i], sigs[96 * i:96 * i + 96], pk_indices=[keys[i]]) for i in range(n)]
+    want = [1] * n
+    wrong = [0, 64 * 2 + 63, 64 * 5 + 20, 64 * 9 + 7, 64 * 9 + 50, 64 * 30 + 1]
+    for i in wrong:
+        sets[i] = native.SetSpec(roots[i], sets[i].sig, pk_indices=[(keys[i] + 1) % NKEYS])
+        want[i] = 0
+    i = 64 * 5 + 21  # undecodable beside the wrong key of group 5
+    sets[i] = native.SetSpec(roots[i], bytes([sets[i].sig[0] & 0x7F]) + sets[i].sig[1:], pk_indices=[keys[i]])
+    want[i] = -native.BLST_BAD_ENCODING
+    jobs = [([s], True) for s in sets]
+    st = native.BgvStats()
+    got = one.verify_jobs(jobs, native.MODE_WORKER, stats=st)
+    assert got == want
+    assert st.batch_retries >= 5
