@@ -120,19 +120,14 @@ static bool uniform_enabled() {
   }();
   return v;
 }
-// A failing group's first retry test is one weighted test (call_build_parts): BGV_WEIGHTED_UNIFORM=0
-// / BGV_WEIGHTED_MIXED=0 take the pattern tests at once instead for uniform groups / the others,
-// for A/B measurements
-static bool weighted_enabled(bool uniform_group) {
-  static const bool u = [] {
+// BGV_WEIGHTED_UNIFORM=0: failing uniform groups take the pattern tests at once (no weighted
+// test first; call_build_parts), for A/B measurements
+static bool weighted_uniform_enabled() {
+  static const bool v = [] {
     const char* e = getenv("BGV_WEIGHTED_UNIFORM");
     return !(e && atoi(e) == 0);
   }();
-  static const bool m = [] {
-    const char* e = getenv("BGV_WEIGHTED_MIXED");
-    return !(e && atoi(e) == 0);
-  }();
-  return uniform_group ? u : m;
+  return v;
 }
 // calls with fewer batchable one-set jobs take the latency path: their jobs keep their order
 #define BGV_UNIFORM_MIN_JOBS 1024
@@ -1092,7 +1087,7 @@ static bool unit_in_group(const Call* call, const std::vector<size_t>& jobs, int
 // Group testing for one retry round: split every pending unit into parts.  gb: the call's
 // first group in the batch when the first pass's u values are on the device (pattern tests
 // possible), else -1.
-static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb, bool uniform, bool weighted) {
+static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb, bool uniform) {
   // A test inside a uniform first-pass group (whose slots have no own pair f_i) pairs the sum
   // of its slots' r_i pk_i with the group's one H instead: prod_S e(r_i pk_i, H) =
   // e(sum_S r_i pk_i, H), the same pairing value, so the complement verdicts hold too
@@ -1104,13 +1099,12 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
     const int ug = call->unit_group[ui], urounds = call->unit_rounds[ui];
     const bool in_group = unit_in_group(call, u, ug);
     const bool eligible = gb >= 0 && in_group && urounds <= 0 && u.size() >= 2 && pattern_eligible(call, ui);
-    if (eligible && urounds == 0 && weighted && weighted_enabled(uflag((uint32_t)ug) != 0)) {
-      // a failing group mostly holds ONE invalid slot (at 1 % invalid sets, ~72 % of failing
-      // 64-set groups; a wrong key in a uniform group almost always): one test with slot k
-      // weighted by k + 1 names it (BGV_GROUP_WEIGHTED; k_final_wident finds w with V^w = W)
-      // instead of ~6 pattern tests; otherwise the pattern tests follow (unit_rounds -1).  Two or
-      // more invalid slots match some w <= 64 only with negligible probability (their values
-      // are independent elements of prime order r).
+    if (eligible && urounds == 0 && uflag((uint32_t)ug) && weighted_uniform_enabled()) {
+      // a failing uniform group almost always holds ONE invalid slot (a wrong key): one test with
+      // slot k weighted by k + 1 names it (BGV_GROUP_WEIGHTED; k_final12 finds w with V^w = W)
+      // instead of ~6 pattern tests of two Miller loops each; otherwise the pattern tests follow
+      // (unit_rounds -1).  Two or more invalid slots match some w <= 64 only with negligible
+      // probability (their values are independent elements of prime order r).
       PatternUnit pu;
       pu.group = (uint32_t)ug;
       pu.kind = 2;
@@ -1129,7 +1123,7 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
       part.pattern = (int)call->punits.size();
       pu.tests.push_back((uint32_t)rg.size());
       rg.push_back(bgv_dgroup{call->slot_base + g.first_slot, g.n_slots, m, (uint32_t)(gb + ug + 1),
-                              uflag((uint32_t)ug) | BGV_GROUP_WEIGHTED});
+                              BGV_GROUP_UNIFORM | BGV_GROUP_WEIGHTED});
       call->parts.push_back(std::move(part));
       call->punits.push_back(std::move(pu));
       continue;
@@ -1577,9 +1571,7 @@ static int retry_launch(Device& d, RetryRun& r, bool* more) {
   const auto th = std::chrono::steady_clock::now();
   std::vector<bgv_dgroup> rg;
   for (size_t k = 0; k < calls.size(); ++k)
-    // weighted tests need the bulk closing (k_final12 + k_final_wprod / k_final_wident)
-    call_build_parts(calls[k], rg, bs.want_gu ? (int64_t)bs.call_gb[k] : -1, bs.uniform,
-                     bs.nslots > bgv_fold_pairs_max());
+    call_build_parts(calls[k], rg, bs.want_gu ? (int64_t)bs.call_gb[k] : -1, bs.uniform);
   *more = !rg.empty();
   r.nrg = 0;
   if (rg.empty()) return BGV_OK;

@@ -90,8 +90,8 @@ __device__ __forceinline__ void final12_body(BGV_FINAL12_ARGS) {
   // present ones only (a retry test masks half of a group or a single job), the teams of the
   // wave to the longest list, multiplying by 1 past their own
   uint64_t m = live ? g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1)) : 0;
-  const bool uni = gpkp && live && (g.flags & (BGV_GROUP_UNIFORM | BGV_GROUP_WEIGHTED));
-  if (uni) m = 0;  // its slots' pairs are the one value gpkp[gi] (a pubkey-sum pair, or k_final_wprod's)
+  const bool uni = gpkp && live && (g.flags & BGV_GROUP_UNIFORM);
+  if (uni) m = 0;  // its slots' pairs are the one pair gpkp[gi]
   if (c == 0) lens[team] = (uint32_t)__popcll(m);
   __syncthreads();
   uint32_t nmax = 0;
@@ -120,44 +120,6 @@ __device__ __forceinline__ void final12_body(BGV_FINAL12_ARGS) {
   if (gu && live) reinterpret_cast<fp_t*>(gu + gi)[fi] = u;
   const int32_t v = verdict_bits(o, u, g, gu1, fi);
   if (live && c == 0) verdict[gi] = v;
-}
-
-// A weighted test over a group without one root (BGV_GROUP_WEIGHTED, not UNIFORM): its slots'
-// own pairs raised to their weights, prod_k f_k^(k + 1) = prod_t S_t with S_t = prod_{k >= t} f_k
-// (two products per slot), into gpkp for the closing.  Teams of 12 lanes as k_final12, each
-// block's teams running to its longest group (the barriers inside o.mul).
-extern "C" __global__ void __launch_bounds__(64) k_final_wprod(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
-                                                               const fp12_t* __restrict__ f, fp12_t* __restrict__ gpkp) {
-  __shared__ fp_t lds[BGV_FINAL12_TEAMS + 1][2 * BGV_TEAM_COMPS];
-  __shared__ uint32_t lens[BGV_FINAL12_TEAMS + 1];
-  const int team = threadIdx.x / BGV_TEAM_COMPS, c = threadIdx.x % BGV_TEAM_COMPS;
-  const uint32_t gi = blockIdx.x * BGV_FINAL12_TEAMS + team;
-  const bool live = team < BGV_FINAL12_TEAMS && gi < ngroups;
-  const bgv_dgroup g = groups[live ? gi : ngroups - 1];
-  const bool wt = live && (g.flags & BGV_GROUP_WEIGHTED) && !(g.flags & BGV_GROUP_UNIFORM);
-  if (c == 0) lens[team] = wt ? g.n_slots : 0u;
-  if (!__syncthreads_or(wt ? 1 : 0)) return;  // the whole block: no such test
-  uint32_t nmax = 0;
-  BGV_UNROLL for (int t = 0; t <= BGV_FINAL12_TEAMS; ++t) nmax = lens[t] > nmax ? lens[t] : nmax;
-  const int fi = tm_fp_index(c);
-  const fp_t one_c = c == 0 ? fp_one() : fp_zero();
-  tm_dev_ops_t<BGV_TEAM_COMPS> o{lds[team], lds[team] + BGV_TEAM_COMPS, c, c};
-  const fp_t* fs = reinterpret_cast<const fp_t*>(f + g.first_slot);
-  constexpr int kFp12 = (int)(sizeof(fp12_t) / sizeof(fp_t));
-  const uint64_t m = g.mask & (g.n_slots >= 64 ? ~0ull : ((1ull << g.n_slots) - 1));
-  fp_t S = one_c, x = one_c;
-  uint32_t k = wt ? g.n_slots : 0;
-  BGV_NO_UNROLL for (uint32_t step = 0; step < nmax; ++step) {
-    const bool more = k > 0;  // a team past its first slot multiplies by 1
-    fp_t y = one_c;
-    if (more) {
-      --k;
-      if ((m >> k) & 1) y = fs[kFp12 * k + fi];
-    }
-    S = o.mul(S, y);
-    x = o.mul(x, more ? S : one_c);
-  }
-  if (wt) reinterpret_cast<fp_t*>(gpkp + gi)[fi] = x;
 }
 
 // Weighted tests (BGV_GROUP_WEIGHTED) after k_final12 of a retry round: the first w <= n_slots
@@ -363,9 +325,6 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     return !(e && atoi(e) == 0);
   }();
   if (b.weighted && !b.gu) return hipErrorInvalidValue;
-  if (b.weighted)  // the weighted products of the tests without one root, before their closing
-    hipLaunchKernelGGL(k_final_wprod, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
-                       b.ngroups, static_cast<const fp12_t*>(b.f), b.gpkp);
   if (b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
@@ -374,7 +333,7 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1,
-                       b.uniform || b.weighted ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
+                       b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
   if (b.weighted)
     hipLaunchKernelGGL(k_final_wident, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, static_cast<const fp12_t*>(b.gu), b.gu1, b.verdict);

@@ -141,21 +141,18 @@ __global__ void __launch_bounds__(64) k_gsum_w(const bgv_dgroup* __restrict__ gr
       }
     }
     g2_jac acc = weighted_lane_sum(ps, c);
-    g1_jac pa = jac_infinity<fp_t>();
-    if (g.flags & BGV_GROUP_UNIFORM) {  // the pubkey side only for a group with one root (team-uniform)
-      pa = weighted_lane_sum(pk, c);
-      pa = jac_add(pa, point_xor<8>(pa));
-      pa = jac_add(pa, point_xor<4>(pa));
-      pa = jac_add(pa, point_xor<2>(pa));
-      pa = jac_add(pa, point_xor<1>(pa));
-    }
+    g1_jac pa = weighted_lane_sum(pk, c);
+    pa = jac_add(pa, point_xor<8>(pa));
+    pa = jac_add(pa, point_xor<4>(pa));
+    pa = jac_add(pa, point_xor<2>(pa));
+    pa = jac_add(pa, point_xor<1>(pa));
     acc = jac_add(acc, point_xor<8>(acc));
     acc = jac_add(acc, point_xor<4>(acc));
     acc = jac_add(acc, point_xor<2>(acc));
     acc = jac_add(acc, point_xor<1>(acc));
     if (gi < ngroups && c == 0) {
       gsum[gi] = acc;
-      if (gpk && (g.flags & BGV_GROUP_UNIFORM)) gpk[gi] = pa;  // the pubkey side of a uniform test
+      if (gpk) gpk[gi] = pa;
     }
     return;
   }
