@@ -405,15 +405,6 @@ static void launch_miller_latency(const bgv_dev_batch& b, uint32_t nslots, uint3
                        static_cast<const g1_jac*>(nullptr), static_cast<fp12_t*>(nullptr));
 }
 
-// BGV_UGPAIR_TEAM=1: uniform batches' group pairs on k_miller_team too (A/B)
-static bool ugpair_team() {
-  static const bool v = [] {
-    const char* e = getenv("BGV_UGPAIR_TEAM");
-    return e && atoi(e) > 0;
-  }();
-  return v;
-}
-
 // lanes of one k_miller round: one wave of 64 on each SIMD (MI355X: 256 CUs x 4 SIMDs)
 static uint32_t miller_round_lanes() {
   static const uint32_t lanes = [] {
@@ -453,7 +444,7 @@ hipError_t bgv_launch_miller(const bgv_dev_batch& b, const bgv_streams& s) {
   if (bgv_use_latency(b, n + b.ngroups)) {
     launch_miller_latency(b, n, b.ngroups, s.main);
   } else if (b.path != BGV_PATH_BULK && b.ngroups <= bgv_latency_max() &&
-             (n + b.ngroups + R - 1) / R > (n + R - 1) / R && (!b.uniform || ugpair_team())) {
+             (n + b.ngroups + R - 1) / R > (n + R - 1) / R && !b.uniform) {
     // the group pairs on extra k_facc lanes would open one more round of one wave per SIMD
     // (131,072 sets + 2,048 groups: 3 rounds instead of 2); run them on teams instead.  Not
     // with uniform groups: their slot lanes exit at once, so no round is full anyway
