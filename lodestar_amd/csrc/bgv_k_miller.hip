@@ -50,33 +50,37 @@ __global__ void BGV_KATTR k_gpair(uint32_t ngroups, const g2_jac* __restrict__ g
   if (g < ngroups) gpair[g] = group_pair(gsum + g);
 }
 
+}  // extern "C"
+// A lane's share of sum_k (k + 1) P_k over slots k = c + 16 t (t = 0..3) of its team:
+// (c + 1) A + 16 B with A = sum_t P_t and B = sum_t t P_t = S1 + S2 + S3, the suffix sums
+// S_t = sum_{t' >= t} P_t' taken from t = 3 down (no array of points: the kernel's stack frame
+// stays that of its point additions).  load(t) returns P_t (infinity for a dead or absent slot).
+template <class P, class Load>
+__device__ P weighted_lane_sum(int c, Load load) {
+  using F = decltype(P{}.x);
+  P S = jac_infinity<F>(), B = jac_infinity<F>();
+  BGV_NO_UNROLL for (int t = 3; t >= 0; --t) {
+    S = jac_add(S, load(t));
+    if (t >= 1) B = jac_add(B, S);
+  }
+  BGV_UNROLL for (int i = 0; i < 4; ++i) B = jac_dbl(B);  // 16 B
+  P r = jac_infinity<F>();
+  const uint32_t w = (uint32_t)c + 1;  // <= 16: five bits, the same loop shape on every lane
+  BGV_NO_UNROLL for (int bit = 4; bit >= 0; --bit) {
+    r = jac_dbl(r);
+    const P ra = jac_add(r, S);
+    r = ((w >> bit) & 1) ? ra : r;
+  }
+  return jac_add(r, B);
+}
+extern "C" {
+
 // S_g = sum of r_i sig_i over a group's live, non-infinity signatures (blst skips an
 // infinity signature in the accumulator).  A team of 16 lanes per group: lane c sums
 // every 16th slot, then a 4-level ds_swizzle butterfly; the team leader writes S_g.
 // A uniform group (BGV_GROUP_UNIFORM: a first-pass group, or a retry test inside one) also sums
 // its live slots' r_i pk_i into gpk: its set pairs are then one pair e(gpk, H) (the same slots
 // k_facc would pair).
-// A lane's share of sum_k (k + 1) P_k over slots k = c + 16 t (t = 0..3) of its team:
-// (c + 1) A + 16 B with A = sum_t P_t and B = sum_t t P_t = S1 + S2 + S3 (S_t the suffix sums).
-// dead / absent slots are infinity.
-}  // extern "C"
-template <class P>
-__device__ P weighted_lane_sum(const P (&pt)[4], int c) {
-  const P s3 = pt[3], s2 = jac_add(pt[2], s3), s1 = jac_add(pt[1], s2);
-  const P a = jac_add(pt[0], s1);
-  P b = jac_add(jac_add(s1, s2), s3);
-  BGV_UNROLL for (int i = 0; i < 4; ++i) b = jac_dbl(b);  // 16 B
-  P r = jac_infinity<decltype(a.x)>();
-  const uint32_t w = (uint32_t)c + 1;  // <= 16: five bits, the same loop shape on every lane
-  BGV_UNROLL for (int bit = 4; bit >= 0; --bit) {
-    r = jac_dbl(r);
-    const P ra = jac_add(r, a);
-    r = ((w >> bit) & 1) ? ra : r;
-  }
-  return jac_add(r, b);
-}
-extern "C" {
-
 __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                              const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
                                              const int32_t* __restrict__ sig_status,
@@ -125,36 +129,36 @@ __global__ void __launch_bounds__(64) k_gsum_w(const bgv_dgroup* __restrict__ gr
   const uint32_t gi = blockIdx.x * BGV_FINAL_TEAMS + team;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
   if (!(g.flags & BGV_GROUP_WEIGHTED)) return;  // k_gsum's (uniform over the team)
-  {
-    g2_jac ps[4];
-    g1_jac pk[4];
-    BGV_UNROLL for (int t = 0; t < 4; ++t) {
-      const uint32_t k = (uint32_t)c + BGV_TEAM * t;
-      ps[t] = jac_infinity<fp2_t>();
-      pk[t] = jac_infinity<fp_t>();
-      if (k < g.n_slots && grp_has(g, k)) {
-        const uint32_t s = g.first_slot + k;
-        const int32_t ss = sig_status[s];
-        const bool live = slot_live(slots[s], ss, pk_status[s]);
-        if (ss == BGV_ST_OK && live) ps[t] = rsig[s];
-        if (live) pk[t] = rpk[s];
-      }
-    }
-    g2_jac acc = weighted_lane_sum(ps, c);
-    g1_jac pa = weighted_lane_sum(pk, c);
+  auto live_at = [&](int t, bool* sig_ok) {  // slot t of the lane takes part; *sig_ok: its signature too
+    const uint32_t k = (uint32_t)c + BGV_TEAM * t;
+    *sig_ok = false;
+    if (k >= g.n_slots || !grp_has(g, k)) return false;
+    const uint32_t s = g.first_slot + k;
+    const int32_t ss = sig_status[s];
+    const bool live = slot_live(slots[s], ss, pk_status[s]);
+    *sig_ok = live && ss == BGV_ST_OK;
+    return live;
+  };
+  g2_jac acc = weighted_lane_sum<g2_jac>(c, [&](int t) {
+    bool ok;
+    live_at(t, &ok);
+    return ok ? rsig[g.first_slot + c + BGV_TEAM * t] : jac_infinity<fp2_t>();
+  });
+  acc = jac_add(acc, point_xor<8>(acc));
+  acc = jac_add(acc, point_xor<4>(acc));
+  acc = jac_add(acc, point_xor<2>(acc));
+  acc = jac_add(acc, point_xor<1>(acc));
+  if (gi < ngroups && c == 0) gsum[gi] = acc;
+  if (g.flags & BGV_GROUP_UNIFORM) {  // the pubkey side of a test with one root (team-uniform)
+    g1_jac pa = weighted_lane_sum<g1_jac>(c, [&](int t) {
+      bool ok;
+      return live_at(t, &ok) ? rpk[g.first_slot + c + BGV_TEAM * t] : jac_infinity<fp_t>();
+    });
     pa = jac_add(pa, point_xor<8>(pa));
     pa = jac_add(pa, point_xor<4>(pa));
     pa = jac_add(pa, point_xor<2>(pa));
     pa = jac_add(pa, point_xor<1>(pa));
-    acc = jac_add(acc, point_xor<8>(acc));
-    acc = jac_add(acc, point_xor<4>(acc));
-    acc = jac_add(acc, point_xor<2>(acc));
-    acc = jac_add(acc, point_xor<1>(acc));
-    if (gi < ngroups && c == 0) {
-      gsum[gi] = acc;
-      if (gpk) gpk[gi] = pa;
-    }
-    return;
+    if (gi < ngroups && c == 0 && gpk) gpk[gi] = pa;
   }
 }
 
