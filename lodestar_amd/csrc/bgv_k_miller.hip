@@ -119,7 +119,8 @@ __global__ void __launch_bounds__(64) k_gsum(const bgv_dgroup* __restrict__ grou
 
 // The weighted tests' sums (BGV_GROUP_WEIGHTED: a whole uniform group, slot k weighted by k + 1):
 // sum (k + 1) r_k sig_k into gsum and sum (k + 1) r_k pk_k into gpk, one team of 16 lanes per
-// group as k_gsum.  A kernel of its own: its point arrays would give k_gsum a 7 KB stack frame.
+// group as k_gsum.  A kernel of its own: its doublings would give k_gsum a 3 KB stack frame
+// (256 B alone).
 __global__ void __launch_bounds__(64) k_gsum_w(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                                const bgv_dslot* __restrict__ slots, const g2_jac* __restrict__ rsig,
                                                const int32_t* __restrict__ sig_status,
