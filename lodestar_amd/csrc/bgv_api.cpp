@@ -135,6 +135,13 @@ static bool weighted_uniform_enabled() {
 // Retry threads per device (BGV_RETRY_THREADS), each with its own high-priority stream: the
 // retry rounds of several super-batches then run side by side instead of queueing behind one
 // another (their rounds are latency-bound chains of small launches)
+// batches a retry thread holds at once (BGV_RETRY_HOLD): 1, one batch's rounds at a time.
+// Holding up to 8 (their rounds side by side, one wait per pass) measured 2.11-2.51 against
+// 2.44-2.46 M sets/s, interleaved (profiles/r05/retry_hold/): the steadier one is the default.
+static size_t retry_hold_max() {
+  static const size_t v = env_size("BGV_RETRY_HOLD", 1, 1);
+  return v;
+}
 static int retry_threads_per_device() {
   static const int v = (int)env_size("BGV_RETRY_THREADS", 1, 1);
   return v;
@@ -1678,7 +1685,7 @@ static void finish_calls(std::vector<Call*>& calls, int rc) {
 
 // The device's retry thread: the retry rounds of handed-over super-batches, in order; drains
 // the queue before it stops.
-// The retry thread holds every batch handed over so far and runs their rounds side by side: each
+// The retry thread holds up to retry_hold_max() handed-over batches and runs their rounds side by side: each
 // pass launches one round of every held batch on the thread's stream, waits once, and applies
 // the verdicts; a batch joins at the next pass after its hand-over and leaves (its calls
 // finished, its Exec released) when it has no parts left.  Under load, when hand-overs queue up,
@@ -1699,7 +1706,7 @@ static void retry_loop(bgv_ctx* c, Device* d, int k) {
       std::unique_lock<std::mutex> lk(s.mu);
       if (held.empty()) s.cv.wait(lk, [&s] { return s.stop || !s.rq.empty(); });
       if (held.empty() && s.rq.empty()) return;  // stopping, and the queue is drained
-      while (!s.rq.empty()) {
+      while (!s.rq.empty() && held.size() < retry_hold_max()) {
         RetryRun r;
         r.job = std::move(s.rq.front());
         s.rq.pop_front();
