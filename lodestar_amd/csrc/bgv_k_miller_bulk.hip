@@ -31,6 +31,11 @@
 #endif
 // (Hand-scheduled exact-clobber product subroutines measured equal at the kernel level,
 // profiles/r04/asm_ab: k_miller 10.69-10.76 vs 10.71-10.86 ms; kept in tools/experimental/.)
+// Fp2 products with deferred reduction (bls_wide.h); k_lines and k_facc run 64-thread blocks,
+// as the products' per-lane LDS operand slot requires
+#ifndef BGV_LZ2_CLASSIC
+#define BGV_LZ2_WIDE 1
+#endif
 #include "bgv_device.h"
 
 #ifndef BGV_WPE_LINES

@@ -4,6 +4,11 @@
 //
 //   k_prep  three independent tasks side by side (blockIdx.y): hash (H(m_i)), sig (decode,
 //           subgroup check, r_i * sig_i) and pk (aggregate, r_i * pk_i); see bgv_k_tasks.h
+// Fp2 products with deferred reduction (bls_wide.h); every kernel of this unit runs 64-thread
+// blocks, as the products' per-lane LDS operand slot requires
+#ifndef BGV_LZ2_CLASSIC
+#define BGV_LZ2_WIDE 1
+#endif
 #include "bgv_k_tasks.h"
 
 // waves per SIMD the bulk k_prep is register-budgeted for (1: 512 registers, 2: 256)

@@ -21,6 +21,7 @@
 // every bound at run time.
 #pragma once
 #include "bls_field.h"
+#include "bls_wide.h"
 
 namespace lzc {
 constexpr uint64_t P13 = 0x1a011;  // top limb of p
@@ -344,7 +345,7 @@ BGV_HD auto lz2_mul_xi(const lz2<LA, VA>& a) {
 }
 // Karatsuba: 3 products, the cross term as (a0 + a1)(b0 + b1) - (t0 + t1)
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
-BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
+BGV_HD auto lz2_mul_c(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
   const lzr t0 = lz_mul(a.c0, b.c0);
   const lzr t1 = lz_mul(a.c1, b.c1);
   const lzr t2 = lz_mul(lz_add(a.c0, a.c1), lz_add(b.c0, b.c1));
@@ -352,13 +353,115 @@ BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
 }
 // (a0 + a1)(a0 - a1), 2 a0 a1: two products, outputs < 2p normalized
 template <uint64_t LA, uint64_t VA>
-BGV_HD lz2r lz2_sqr(const lz2<LA, VA>& a) {
+BGV_HD lz2r lz2_sqr_c(const lz2<LA, VA>& a) {
   return lz2r{lz_mul(lz_add(a.c0, a.c1), lz_sub(a.c0, a.c1)), lz_mul(lz_dbl(a.c0), a.c1)};
 }
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
-BGV_HD lz2r lz2_mul_fp(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
+BGV_HD lz2r lz2_mul_fp_c(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
   return lz2r{lz_mul(a.c0, s), lz_mul(a.c1, s)};
 }
+
+// The deferred-reduction forms (bls_wide.h): one out-of-line call per Fp2 operation, b (or s)
+// through the lane's LDS slot.  Same field elements as the _c forms (tests/test_wide.py).
+BGV_HD lz2<LMASK, 2> lz2_unpack(const bgv_u28& r) {
+  lz2<LMASK, 2> o;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    o.c0.v[i] = r[i];
+    o.c1.v[i] = r[NL + i];
+  }
+  return o;
+}
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD lz2<LMASK, 3> lz2_mul_w(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
+  static_assert(bgvw::mul_ok(LA, LB), "lz2_mul_w: limb product overflows the column sums");
+  static_assert(VA * VB <= lzc::VMUL_MAX, "lz2_mul_w: operand values too large for a < 3p result");
+  uint32_t w[2 * NL];
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    w[i] = b.c0.v[i];
+    w[NL + i] = b.c1.v[i];
+  }
+  wslot_put(w, 2 * NL);
+  const bgv_u28 r = fp2_mul_w_l(BGV_V14(a.c0), BGV_V14(a.c1));
+  lz2<LMASK, 3> o;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    o.c0.v[i] = r[i];
+    o.c1.v[i] = r[NL + i];
+  }
+  LZ_CHECK(o.c0, "mul_w re");
+  LZ_CHECK(o.c1, "mul_w im");
+  return o;
+}
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD lz2r lz2_mul_fp_w(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
+  static_assert(bgvw::mul2_ok(LA, LB), "lz2_mul_fp_w: limb product overflows the column sums");
+  static_assert(VA * VB < lzc::VMUL_MAX, "lz2_mul_fp_w: operand values too large for a < 2p result");
+  wslot_put(s.v, NL);
+  const bgv_u28 r = fp2_mul_fp_w_l(BGV_V14(a.c0), BGV_V14(a.c1));
+  const lz2r o = lz2_unpack(r);
+  LZ_CHECK(o.c0, "mul_fp_w re");
+  LZ_CHECK(o.c1, "mul_fp_w im");
+  return o;
+}
+struct lz_wsqr {
+  static constexpr lzc::kp K = lzc::make_kp(BGV_WSQR_LIMB, BGV_WSQR_V);
+  static_assert(K.k != 0, "lz_wsqr: no k p representation");
+  static_assert(bgvw::mul2_ok(2 * BGV_WSQR_LIMB, BGV_WSQR_LIMB + K.maxl), "lz_wsqr: column sums overflow");
+  static_assert(2 * BGV_WSQR_V * (BGV_WSQR_V + K.k) < lzc::VMUL_MAX, "lz_wsqr: value bound");
+};
+BGV_MUL_ATTR bgv_u28 fp2_sqr_w_l(BGV_U14(a0_), BGV_U14(a1_)) {
+  BGV_COUNT_SQR();
+  BGV_COUNT_SQR();
+  const uint32_t a0[NL] = {BGV_L14(a0_)}, a1[NL] = {BGV_L14(a1_)};
+  uint32_t kp[NL], r0[NL], r1[NL];
+  BGV_UNROLL for (int i = 0; i < NL; ++i) kp[i] = lz_wsqr::K.v[i];
+  fp2_sqr_w_body(a0, a1, kp, r0, r1);
+  return w28_pack(r0, r1);
+}
+template <uint64_t LA, uint64_t VA>
+BGV_HD lz2r lz2_sqr_w(const lz2<LA, VA>& a) {
+  static_assert(LA <= BGV_WSQR_LIMB && VA <= BGV_WSQR_V, "lz2_sqr_w: operand out of the squaring's bounds");
+  const lz2r o = lz2_unpack(fp2_sqr_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
+  LZ_CHECK(o.c0, "sqr_w re");
+  LZ_CHECK(o.c1, "sqr_w im");
+  return o;
+}
+
+#if defined(BGV_LZ2_WIDE)
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
+  if constexpr (bgvw::mul_ok(LA, LB) && VA * VB <= lzc::VMUL_MAX)
+    return lz2_mul_w(a, b);
+  else
+    return lz2_mul_c(a, b);
+}
+template <uint64_t LA, uint64_t VA>
+BGV_HD lz2r lz2_sqr(const lz2<LA, VA>& a) {
+  if constexpr (LA <= BGV_WSQR_LIMB && VA <= BGV_WSQR_V)
+    return lz2_sqr_w(a);
+  else
+    return lz2_sqr_c(a);
+}
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD lz2r lz2_mul_fp(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
+  if constexpr (bgvw::mul2_ok(LA, LB) && VA * VB < lzc::VMUL_MAX)
+    return lz2_mul_fp_w(a, s);
+  else
+    return lz2_mul_fp_c(a, s);
+}
+#else
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
+  return lz2_mul_c(a, b);
+}
+template <uint64_t LA, uint64_t VA>
+BGV_HD lz2r lz2_sqr(const lz2<LA, VA>& a) {
+  return lz2_sqr_c(a);
+}
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+BGV_HD lz2r lz2_mul_fp(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
+  return lz2_mul_fp_c(a, s);
+}
+#endif
 template <uint64_t LA, uint64_t VA>
 BGV_HD lz2<LA, VA> lz2_sel(bool c, const lz2<LA, VA>& a, const lz2<LA, VA>& b) {
   return lz2<LA, VA>{lz_sel(c, a.c0, b.c0), lz_sel(c, a.c1, b.c1)};

@@ -6,27 +6,37 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "native", "hostsim.cpp")
-LIB = os.path.join(HERE, "native", "libhostsim.so")
 CSRC = os.path.join(os.path.dirname(HERE), "lodestar_amd", "csrc")
+# Two host builds of the same math: "wide" with the deferred-reduction Fp2 products the bulk
+# kernel units use (bls_wide.h, -DBGV_LZ2_WIDE), "classic" with the fully reduced Karatsuba the
+# other units use.
+VARIANTS = {"wide": ["-DBGV_LZ2_WIDE"], "classic": []}
+LIB = os.path.join(HERE, "native", "libhostsim.so")
 
 
-def build(force=False):
+def lib_path(variant="wide"):
+    return LIB if variant == "wide" else os.path.join(HERE, "native", "libhostsim_%s.so" % variant)
+
+
+def build(force=False, variant="wide"):
+    out = lib_path(variant)
     deps = [SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in deps):
-        return LIB
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     # -DBGV_LAZY_CHECK: every lazy value (bls_lazy.h) is checked against its static bounds
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-DBGV_LAZY_CHECK", "-shared", "-fPIC", "-o", LIB, SRC])
-    return LIB
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-DBGV_LAZY_CHECK", "-shared", "-fPIC", "-o", out + ".tmp", SRC]
+                          + VARIANTS[variant])
+    os.replace(out + ".tmp", out)
+    return out
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        _lib = ctypes.CDLL(build())
-    return _lib
+def lib(variant="wide"):
+    if variant not in _libs:
+        _libs[variant] = ctypes.CDLL(build(variant=variant))
+    return _libs[variant]
 
 
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB

@@ -417,4 +417,67 @@ int hs_g1_decompress(uint8_t* out, const uint8_t* in48) {
   return 0;
 }
 void hs_g1_serialize(uint8_t* out96, const uint8_t* aff) { g1_serialize(out96, in_g1(aff), false); }
+// ---- deferred-reduction Fp2 products (bls_wide.h) against the fully reduced Karatsuba ----
+// n random operand pairs per bound pair and the extreme ones (every limb at its bound, the top
+// limb as high as the value bound allows, zero); both results reduced and compared mod p.
+extern "C++" {
+static uint64_t hs_rng_state;
+static uint64_t hs_rng() {
+  hs_rng_state ^= hs_rng_state << 13;
+  hs_rng_state ^= hs_rng_state >> 7;
+  hs_rng_state ^= hs_rng_state << 17;
+  return hs_rng_state;
+}
+template <uint64_t L, uint64_t V>
+static lz<L, V> hs_lz(int kind) {
+  lz<L, V> r;
+  const uint32_t top = (uint32_t)((V - 1) * (lzc::P13 + 1) < L ? (V - 1) * (lzc::P13 + 1) : L);
+  for (int i = 0; i < NL; ++i) {
+    if (kind == 0) r.v[i] = (uint32_t)(hs_rng() % (L + 1));
+    else if (kind == 1) r.v[i] = (uint32_t)L;
+    else r.v[i] = 0;
+  }
+  r.v[NL - 1] = kind == 0 ? (uint32_t)(hs_rng() % (top + 1)) : (kind == 1 ? top : 0);
+  LZ_CHECK(r, "hs_lz");
+  return r;
+}
+template <uint64_t L, uint64_t V>
+static bool hs_same(const lz<L, V>& a, const lz<LMASK, 2>& b) {
+  const fp_t x = fp_canon(lz_out(lz_norm(a))), y = fp_canon(lz_out(b));
+  return memcmp(x.v, y.v, sizeof(x.v)) == 0;
+}
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+static int hs_wide_pair(int n) {
+  int bad = 0;
+  for (int t = 0; t < n + 9; ++t) {
+    const int ka = t < n ? 0 : (t - n) / 3, kb = t < n ? 0 : (t - n) % 3;
+    const lz2<LA, VA> a{hs_lz<LA, VA>(ka), hs_lz<LA, VA>(kb)};
+    const lz2<LB, VB> b{hs_lz<LB, VB>(kb), hs_lz<LB, VB>(ka)};
+    const auto w = lz2_mul_w(a, b);
+    const auto c = lz2_red(lz2_mul_c(a, b));
+    bad += !hs_same(w.c0, c.c0) || !hs_same(w.c1, c.c1);
+    const auto m = lz2_mul_fp_w(a, b.c0);
+    const auto mc = lz2_mul_fp_c(a, b.c0);
+    bad += !hs_same(m.c0, mc.c0) || !hs_same(m.c1, mc.c1);
+  }
+  return bad;
+}
+}  // extern "C++"
+int hs_wide_check(int n, uint64_t seed) {
+  hs_rng_state = seed | 1;
+  int bad = 0;
+  bad += hs_wide_pair<LMASK, 2, LMASK, 2>(n);
+  bad += hs_wide_pair<LMASK, 3, LMASK, 3>(n);
+  bad += hs_wide_pair<(1u << 29) - 1, 4, (1u << 29) - 1, 4>(n);
+  bad += hs_wide_pair<(1u << 29) + (1u << 28), 6, LMASK, 3>(n);
+  bad += hs_wide_pair<LMASK, 20, LMASK, 30>(n);
+  for (int t = 0; t < n + 3; ++t) {  // the squaring at its limb bound
+    const int k = t < n ? 0 : t - n;
+    const lz2<BGV_WSQR_LIMB, BGV_WSQR_V> a{hs_lz<BGV_WSQR_LIMB, BGV_WSQR_V>(k), hs_lz<BGV_WSQR_LIMB, BGV_WSQR_V>(k == 0 ? 0 : 2 - k / 2)};
+    const auto w = lz2_sqr_w(a);
+    const auto c = lz2_sqr_c(a);
+    bad += !hs_same(w.c0, c.c0) || !hs_same(w.c1, c.c1);
+  }
+  return bad;
+}
 }

@@ -25,9 +25,9 @@ def rfp2():
     return (rfp(), rfp())
 
 
-@pytest.fixture(scope="module")
-def L():
-    return hs.lib()
+@pytest.fixture(scope="module", params=["wide", "classic"])
+def L(request):
+    return hs.lib(request.param)
 
 
 def test_fp_ops(L):
@@ -461,3 +461,12 @@ def test_team_final_exp_check(L):
     assert L.hs_team_final_is_one_wide(m.raw) == 0
     assert L.hs_team_final_is_one_wide8(m.raw) == 0
     assert L.hs_team_final_is_one_wide8_lean(m.raw) == 0
+
+
+def test_wide_fp2_products_equal_classic():
+    """bls_wide.h's deferred-reduction Fp2 product, Fp2-by-Fp product and squaring (the bulk
+    kernels' tower, blst mul_mont_384x style) against the fully reduced Karatsuba, mod p: random
+    operands at five bound pairs (normalized up to 2^29 + 2^28 limbs, values up to 30 p) and the
+    extreme ones (every limb at its bound, zero).  The host build also checks every lazy bound."""
+    for variant in ("wide", "classic"):
+        assert hs.lib(variant).hs_wide_check(400, 0xB15 + len(variant)) == 0
