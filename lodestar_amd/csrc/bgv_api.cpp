@@ -610,15 +610,16 @@ static int exec_reserve_groups(Exec& x, uint32_t groups) {
 }
 
 // line records for the batch's bulk Miller launch (none on the latency path): allocated on
-// first use, in steps of 16,384 pairs (374 MB); kept for the next batch up to the default
-// super-batch's pairs, freed after a larger call (a 2^20-set job alone needs ~24 GB:
-// exec_trim_lines)
-static uint32_t lines_keep_pairs() {
-  const size_t slots = max_batch_slots();
+// first use, in steps of 16,384 pairs (374 MB); kept for the next batch up to the context's
+// current super-batch geometry (c->max_slots, which bgv_set_batching may raise above the
+// environment's default: trimming against the default would free and reallocate the records --
+// each hipFree a device synchronization -- after every first pass), freed after a larger call
+// (a 2^20-set job alone needs ~24 GB: exec_trim_lines)
+static uint32_t lines_keep_pairs(size_t slots) {
   return (uint32_t)((slots + slots / BGV_WAVE + 16383u) & ~(size_t)16383u);
 }
-static void exec_trim_lines(Exec& x) {
-  if (x.lines_cap <= lines_keep_pairs()) return;
+static void exec_trim_lines(Exec& x, size_t max_slots) {
+  if (x.lines_cap <= lines_keep_pairs(max_slots)) return;
   (void)hipFree(x.d_lines);
   x.d_lines = nullptr;
   x.lines_cap = 0;
@@ -1224,10 +1225,14 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
           n += call->jobs[part.jobs[q2]].n_sets;
           ++q2;
         }
-        // chunks within one first-pass group each (groups start on wave boundaries), so a chunk
-        // of a uniform group takes its flag
+        // chunks within one first-pass group each, so a chunk of a uniform group takes its flag
+        // and its root: bounded by the end of slot s0's own group (with BGV_GROUP_SLOTS < 64 a
+        // wave holds several groups) and by the wave
         for (uint32_t off = 0; off < n;) {
-          const uint32_t s0 = first + off, len = std::min<uint32_t>(n - off, BGV_WAVE - s0 % BGV_WAVE);
+          const uint32_t s0 = first + off;
+          const bgv_dgroup& g0 = call->L.groups[call->L.slots[s0].group];
+          const uint32_t len = std::min<uint32_t>(std::min<uint32_t>(n - off, BGV_WAVE - s0 % BGV_WAVE),
+                                                  g0.first_slot + g0.n_slots - s0);
           part.groups.push_back((uint32_t)rg.size());
           rg.push_back(bgv_dgroup{call->slot_base + s0, len, BGV_ALL_SLOTS, 0, uflag(call->L.slots[s0].group)});
           off += len;
@@ -1490,7 +1495,7 @@ static int run_pass1(bgv_ctx* c, Device& d, Exec& x, std::vector<Call*>& calls, 
   HIPCHK(hipStreamSynchronize(x.main));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
-  exec_trim_lines(x);  // the records are dead once the first pass is done
+  exec_trim_lines(x, c->max_slots.load());  // the records are dead once the first pass is done
   if (prof) prof_add(c, x, true, true);
   t_pass1 = ms_since(tg);
   const auto tp = std::chrono::steady_clock::now();

@@ -325,7 +325,12 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     return !(e && atoi(e) == 0);
   }();
   if (b.weighted && !b.gu) return hipErrorInvalidValue;
-  if (b.nslots + b.ngroups <= bgv_latency_max())
+  // A retry round of a uniform batch (b.uniform: tests inside uniform first-pass groups, whose
+  // slots have no pair f_i of their own) closes on k_final12, which multiplies the tests' pubkey-
+  // sum pairs (gpkp), whatever its size: its b.ngroups counts only the round's tests, so a batch
+  // just above the latency bound on its first pass can fall below it here (advisor r05), and
+  // k_final_fold would multiply the groups' unwritten f_i instead.
+  if (!b.uniform && b.nslots + b.ngroups <= bgv_latency_max())
     hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,

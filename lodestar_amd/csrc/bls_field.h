@@ -402,8 +402,14 @@ BGV_NOINLINE fp_t fp_pow_fixed(const fp_t& a) {
     const uint32_t st = s.step[ku];
     const int d = (int)(st >> 8), nsq = (int)(st & 0xff);
     const fp_t m = tab[d & 15];
+#if defined(BGV_POW_INLINE)
+    // the chain's products inline (one copy each in the loop): no call per squaring
+    BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) r = fp_sqr_body(r);
+    if (d != 0xff) r = fp_mul_body(r, m);
+#else
     BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) r = fp_sqr(r);
     if (d != 0xff) r = fp_mul(r, m);
+#endif
   }
   return r;
 }
@@ -519,7 +525,16 @@ BGV_HD fp2_t fp2_conj(const fp2_t& a) { return fp2_t{a.c0, fp_neg(a.c1)}; }
 // Operand components: normalized limbs, values < 8p (fp6/fp12 Karatsuba sums made
 // with fp2_add_norm); the operand sums below are then < 16p with limbs < 2^29,
 // within fp_mul_l's bounds.  The result is weakly reduced.
+#if defined(BGV_LZ2_WIDE)
+// a unit with the deferred-reduction Fp2 products (bls_wide.h; defined in bls_lazy.h)
+BGV_HD fp2_t fp2_mul_wide(const fp2_t& a, const fp2_t& b);
+BGV_HD fp2_t fp2_sqr_wide(const fp2_t& a);
+BGV_HD fp2_t fp2_mul_fp_wide(const fp2_t& a, const fp_t& s);
+#endif
 BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+#if defined(BGV_LZ2_WIDE)
+  return fp2_mul_wide(a, b);
+#endif
   fp_t t0 = fp_mul(a.c0, b.c0);
   fp_t t1 = fp_mul(a.c1, b.c1);
   fp_t t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));
@@ -528,6 +543,9 @@ BGV_HD fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
 
 // a weakly reduced (< 2p): (a0 + a1)(a0 - a1 + 2p) and (2 a0) a1, no reduced adds.
 BGV_HD fp2_t fp2_sqr(const fp2_t& a) {
+#if defined(BGV_LZ2_WIDE)
+  return fp2_sqr_wide(a);
+#endif
   return fp2_t{fp_mul(fp_add_nr(a.c0, a.c1), fp_sub_nr(a.c0, a.c1)), fp_mul(fp_add_nr(a.c0, a.c0), a.c1)};
 }
 
@@ -536,7 +554,12 @@ BGV_HD fp2_t fp2_add_norm(const fp2_t& a, const fp2_t& b) {
   return fp2_t{fp_add_norm(a.c0, b.c0), fp_add_norm(a.c1, b.c1)};
 }
 
-BGV_HD fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { return fp2_t{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+BGV_HD fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) {
+#if defined(BGV_LZ2_WIDE)
+  return fp2_mul_fp_wide(a, b);
+#endif
+  return fp2_t{fp_mul(a.c0, b), fp_mul(a.c1, b)};
+}
 
 // multiply by xi = 1 + i
 BGV_HD fp2_t fp2_mul_xi(const fp2_t& a) { return fp2_t{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }

@@ -21,7 +21,6 @@
 // every bound at run time.
 #pragma once
 #include "bls_field.h"
-#include "bls_wide.h"
 
 namespace lzc {
 constexpr uint64_t P13 = 0x1a011;  // top limb of p
@@ -76,6 +75,8 @@ constexpr kp make_kp(uint64_t lb, uint64_t vb) {
   return out;  // k == 0: no representation (static_assert at the use)
 }
 }  // namespace lzc
+
+#include "bls_wide.h"  // after lzc: its fixed k p come from make_kp
 
 template <uint64_t LM, uint64_t VM>
 struct lz {
@@ -362,75 +363,61 @@ BGV_HD lz2r lz2_mul_fp_c(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
 }
 
 // The deferred-reduction forms (bls_wide.h): one out-of-line call per Fp2 operation, b (or s)
-// through the lane's LDS slot.  Same field elements as the _c forms (tests/test_wide.py).
-BGV_HD lz2<LMASK, 2> lz2_unpack(const bgv_u28& r) {
-  lz2<LMASK, 2> o;
+// through the lane's LDS slot.  Same field elements as the _c forms
+// (tests/test_hostsim_math.py::test_wide_fp2_products_equal_classic).
+template <uint64_t V>
+BGV_HD lz2<LMASK, V> lz2_unpack(const bgv_u28& r) {
+  lz2<LMASK, V> o;
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
     o.c0.v[i] = r[i];
     o.c1.v[i] = r[NL + i];
   }
+  LZ_CHECK(o.c0, "wide re");
+  LZ_CHECK(o.c1, "wide im");
   return o;
 }
+// b goes to the slot: its limbs must be within BGV_WMUL_LB and its values within BGV_WMUL_VB p
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
-BGV_HD lz2<LMASK, 3> lz2_mul_w(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
+BGV_HD auto lz2_mul_w(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
   static_assert(bgvw::mul_ok(LA, LB), "lz2_mul_w: limb product overflows the column sums");
-  static_assert(VA * VB <= lzc::VMUL_MAX, "lz2_mul_w: operand values too large for a < 3p result");
+  constexpr uint64_t V = bgvw::mul_vout(VA, VB);
+  static_assert(V != 0, "lz2_mul_w: operand values too large");
   uint32_t w[2 * NL];
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
     w[i] = b.c0.v[i];
     w[NL + i] = b.c1.v[i];
   }
   wslot_put(w, 2 * NL);
-  const bgv_u28 r = fp2_mul_w_l(BGV_V14(a.c0), BGV_V14(a.c1));
-  lz2<LMASK, 3> o;
-  BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    o.c0.v[i] = r[i];
-    o.c1.v[i] = r[NL + i];
-  }
-  LZ_CHECK(o.c0, "mul_w re");
-  LZ_CHECK(o.c1, "mul_w im");
-  return o;
+  return lz2_unpack<V>(fp2_mul_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
 }
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
 BGV_HD lz2r lz2_mul_fp_w(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
   static_assert(bgvw::mul2_ok(LA, LB), "lz2_mul_fp_w: limb product overflows the column sums");
   static_assert(VA * VB < lzc::VMUL_MAX, "lz2_mul_fp_w: operand values too large for a < 2p result");
   wslot_put(s.v, NL);
-  const bgv_u28 r = fp2_mul_fp_w_l(BGV_V14(a.c0), BGV_V14(a.c1));
-  const lz2r o = lz2_unpack(r);
-  LZ_CHECK(o.c0, "mul_fp_w re");
-  LZ_CHECK(o.c1, "mul_fp_w im");
-  return o;
-}
-struct lz_wsqr {
-  static constexpr lzc::kp K = lzc::make_kp(BGV_WSQR_LIMB, BGV_WSQR_V);
-  static_assert(K.k != 0, "lz_wsqr: no k p representation");
-  static_assert(bgvw::mul2_ok(2 * BGV_WSQR_LIMB, BGV_WSQR_LIMB + K.maxl), "lz_wsqr: column sums overflow");
-  static_assert(2 * BGV_WSQR_V * (BGV_WSQR_V + K.k) < lzc::VMUL_MAX, "lz_wsqr: value bound");
-};
-BGV_MUL_ATTR bgv_u28 fp2_sqr_w_l(BGV_U14(a0_), BGV_U14(a1_)) {
-  BGV_COUNT_SQR();
-  BGV_COUNT_SQR();
-  const uint32_t a0[NL] = {BGV_L14(a0_)}, a1[NL] = {BGV_L14(a1_)};
-  uint32_t kp[NL], r0[NL], r1[NL];
-  BGV_UNROLL for (int i = 0; i < NL; ++i) kp[i] = lz_wsqr::K.v[i];
-  fp2_sqr_w_body(a0, a1, kp, r0, r1);
-  return w28_pack(r0, r1);
+  return lz2_unpack<2>(fp2_mul_fp_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
 }
 template <uint64_t LA, uint64_t VA>
 BGV_HD lz2r lz2_sqr_w(const lz2<LA, VA>& a) {
   static_assert(LA <= BGV_WSQR_LIMB && VA <= BGV_WSQR_V, "lz2_sqr_w: operand out of the squaring's bounds");
-  const lz2r o = lz2_unpack(fp2_sqr_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
-  LZ_CHECK(o.c0, "sqr_w re");
-  LZ_CHECK(o.c1, "sqr_w im");
-  return o;
+  return lz2_unpack<2>(fp2_sqr_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
+}
+// which operand of a product can take the slot (0: neither)
+template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
+constexpr int lz2_wide_side() {
+  if constexpr (bgvw::mul_ok(LA, LB) && bgvw::mul_vout(VA, VB) != 0) return 1;
+  if constexpr (bgvw::mul_ok(LB, LA) && bgvw::mul_vout(VB, VA) != 0) return 2;
+  return 0;
 }
 
 #if defined(BGV_LZ2_WIDE)
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
 BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
-  if constexpr (bgvw::mul_ok(LA, LB) && VA * VB <= lzc::VMUL_MAX)
+  constexpr int side = lz2_wide_side<LA, VA, LB, VB>();
+  if constexpr (side == 1)
     return lz2_mul_w(a, b);
+  else if constexpr (side == 2)
+    return lz2_mul_w(b, a);
   else
     return lz2_mul_c(a, b);
 }
@@ -460,6 +447,38 @@ BGV_HD lz2r lz2_sqr(const lz2<LA, VA>& a) {
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
 BGV_HD lz2r lz2_mul_fp(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
   return lz2_mul_fp_c(a, s);
+}
+#endif
+
+// The eager fp2_t products of bls_field.h in a BGV_LZ2_WIDE unit (declared there): operand
+// components normalized (limbs < 2^28) with values < 8p, results weakly reduced (< 2p).
+#if defined(BGV_LZ2_WIDE)
+BGV_HD fp2_t fp2_from_w28(const bgv_u28& r) {
+  fp2_t o;
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    o.c0.v[i] = r[i];
+    o.c1.v[i] = r[NL + i];
+  }
+  return o;
+}
+BGV_HD fp2_t fp2_mul_wide(const fp2_t& a, const fp2_t& b) {
+  static_assert(bgvw::mul_ok(LMASK, LMASK) && bgvw::mul_vout(8, 8) == 2, "fp2_mul_wide: eager bounds");
+  uint32_t w[2 * NL];
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    w[i] = b.c0.v[i];
+    w[NL + i] = b.c1.v[i];
+  }
+  wslot_put(w, 2 * NL);
+  return fp2_from_w28(fp2_mul_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
+}
+BGV_HD fp2_t fp2_sqr_wide(const fp2_t& a) {
+  static_assert(LMASK <= BGV_WSQR_LIMB && 2 <= BGV_WSQR_V, "fp2_sqr_wide: eager bounds");
+  return fp2_from_w28(fp2_sqr_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
+}
+BGV_HD fp2_t fp2_mul_fp_wide(const fp2_t& a, const fp_t& s) {
+  static_assert(bgvw::mul2_ok(LMASK, LMASK) && 8 * 8 < lzc::VMUL_MAX, "fp2_mul_fp_wide: eager bounds");
+  wslot_put(s.v, NL);
+  return fp2_from_w28(fp2_mul_fp_w_l(BGV_V14(a.c0), BGV_V14(a.c1)));
 }
 #endif
 template <uint64_t LA, uint64_t VA>

@@ -11,13 +11,15 @@
 // the same column.  Between columns the only state is two carries and the 2 x 14 reduction
 // digits m_i, so nothing double-width is ever stored.
 //
-//   * S is non-negative column by column ((a0_i + a1_i)(b0_j + b1_j) - a0_i b0_j - a1_i b1_j =
-//     a0_i b1_j + a1_i b0_j), so its stream is unsigned; D's stream is signed (two's
-//     complement columns, arithmetic carries).  Intermediate wrap-around of the unsigned
-//     column sums is harmless: only each column's final value must fit (bls_lazy.h asserts
-//     LA LB against both bounds at every use).
-//   * D may be negative: p R is added to its columns 14..27 (a constant folded into the sums),
-//     so REDC(D) + p lands in (0, 3p) for operand values VA VB <= 2520 = floor(R / p), like S.
+//   * No stream is ever negative: t1 enters both outputs through the negated operand
+//     b1n = k p - b1 (a redundant k p whose limbs cover b1's bound, lzc::make_kp), so
+//     t1' = a1 b1n = k p a1 - a1 b1 and D = t0 + t1', S = t2 - t0 + t1' agree with the
+//     Karatsuba coefficients mod p.  Column by column D and S are sums of non-negative
+//     products (S_k = sum a0_i b1_j + a1_i b0_j + a1_i kp_j), so both streams are unsigned;
+//     intermediate wrap-around of t2 - t0 is harmless, only each column's final value must fit
+//     (bgvw::mul_ok, asserted at every use in bls_lazy.h).
+//   * Values: D < (VA VB + VA k) p^2 and S < (2 VA VB + VA k) p^2, so both results stay
+//     below 2p when those sums are <= 2520 = floor(R / p) (below 3p up to 5040).
 //
 // The out-of-line products take a (the 28 limbs of a0, a1) in VGPR arguments; the AMDGPU
 // calling convention passes at most 32 VGPRs and returns a struct of more than 16 dwords
@@ -76,35 +78,47 @@ inline void wslot_get(uint32_t* w, int n) {
 // ---------------------------------------------------------------------------------------------
 // bodies (also the host reference: tests/native/hostsim.cpp)
 // ---------------------------------------------------------------------------------------------
+// The slot operand's negation b1n = KM - b1 and the squaring's a0 - a1 + KS: fixed redundant
+// multiples of p for the operand bounds the out-of-line entries accept.
+#define BGV_WMUL_LB ((1ull << 29) - 1)
+#define BGV_WMUL_VB 8
+#define BGV_WSQR_LIMB ((1ull << 28) + (1ull << 27))
+#define BGV_WSQR_V 8
 namespace bgvw {
+constexpr lzc::kp KM = lzc::make_kp(BGV_WMUL_LB, BGV_WMUL_VB);
+constexpr lzc::kp KS = lzc::make_kp(BGV_WSQR_LIMB, BGV_WSQR_V);
+static_assert(KM.k != 0 && KS.k != 0, "bls_wide: no k p representation");
 constexpr uint64_t PMAX = 0xfffffffull;  // largest limb of p
-// the largest final column value of an unsigned stream with n_terms operand-limb products of
-// at most lalb each, its 14 reduction terms m_i p_j and the carry in
-constexpr unsigned __int128 col_max(unsigned __int128 lalb, int n_terms) {
-  return lalb * n_terms + (unsigned __int128)14 * LMASK * PMAX + ((unsigned __int128)1 << 37);
-}
-// bounds of fp2_mul_w_body for operand limbs la (a0, a1) and lb (b0, b1)
+typedef unsigned __int128 u128;
+// the largest final column value of a stream whose operand products sum to at most sum_ab per
+// column, plus its 14 reduction terms m_i p_j and the carry in
+constexpr u128 col_max(u128 sum_ab) { return sum_ab + (u128)14 * LMASK * PMAX + ((u128)1 << 37); }
+constexpr u128 TWO64 = (u128)1 << 64;
+// fp2_mul_w_body for a limbs <= la and b limbs <= lb (b in the slot)
 constexpr bool mul_ok(uint64_t la, uint64_t lb) {
-  return 2 * la <= 0xffffffffull && 2 * lb <= 0xffffffffull &&
-         col_max((unsigned __int128)la * lb, 28) < ((unsigned __int128)1 << 64) &&        // S
-         col_max((unsigned __int128)la * lb, 14) + PMAX < ((unsigned __int128)1 << 63);  // |D|
+  return lb <= BGV_WMUL_LB && 2 * la <= 0xffffffffull &&
+         col_max((u128)14 * la * (2 * lb + KM.maxl)) < TWO64 &&  // S
+         col_max((u128)14 * la * (lb + KM.maxl)) < TWO64;        // D
 }
-// bounds of fp_mul2_w_body for operand limbs lx (x, z) and ly (y, w)
-constexpr bool mul2_ok(uint64_t lx, uint64_t ly) {
-  return col_max((unsigned __int128)lx * ly, 14) < ((unsigned __int128)1 << 64);
+// the value bound (in p) of both results for operand values va, vb (b in the slot): 0 if too big
+constexpr uint64_t mul_vout(uint64_t va, uint64_t vb) {
+  const uint64_t m = 2 * va * vb + va * KM.k;
+  return vb > BGV_WMUL_VB ? 0 : (m <= 2520 ? 2 : (m <= 5040 ? 3 : 0));
 }
-}  // namespace bgvw
+// fp_mul2_w_body for x, z limbs <= lx and y, w limbs <= ly
+constexpr bool mul2_ok(uint64_t lx, uint64_t ly) { return col_max((u128)14 * lx * ly) < TWO64; }
+static_assert(mul2_ok(2 * BGV_WSQR_LIMB, BGV_WSQR_LIMB + KS.maxl), "bls_wide: squaring column sums overflow");
+static_assert(2 * BGV_WSQR_V * (BGV_WSQR_V + KS.k) < 2520, "bls_wide: squaring value bound");
 
 // The column loops are compile-time recursions (one instantiation per column k), so every
 // index is a constant and nothing is indexed dynamically: a plain `#pragma unroll` over 27
 // columns with triangular inner loops was left rolled by the compiler (VGPR-indexed arrays).
-namespace bgvw {
 struct mul_state {
   uint32_t sa[NL], sb[NL], md[NL], ms[NL];
-  uint64_t cd, cs;  // cd: a signed carry in two's complement
+  uint64_t cd, cs;
 };
 template <int K>
-BGV_HD void mul_col(mul_state& st, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+BGV_HD void mul_col(mul_state& st, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1n,
                     uint32_t* r0, uint32_t* r1) {
   const uint32_t P_[NL] = BGV_P_LIMBS;
   // the column's product sums and its reduction terms from the earlier digits do not depend on
@@ -115,7 +129,7 @@ BGV_HD void mul_col(mul_state& st, const uint32_t* a0, const uint32_t* a1, const
     const int j = K - i;
     if (j < 0 || j >= NL) continue;
     e += (uint64_t)a0[i] * b0[j];
-    q += (uint64_t)a1[i] * b1[j];
+    q += (uint64_t)a1[i] * b1n[j];
     s += (uint64_t)st.sa[i] * st.sb[j];
   }
   BGV_UNROLL for (int i = 0; i < NL; ++i) {  // oldest digit first: the newest joins last
@@ -124,11 +138,8 @@ BGV_HD void mul_col(mul_state& st, const uint32_t* a0, const uint32_t* a1, const
     dm += (uint64_t)st.md[i] * P_[j];
     sm += (uint64_t)st.ms[i] * P_[j];
   }
-  uint64_t d = (e - q) + dm;
-  s = (s - (e + q)) + sm;
-  if constexpr (K >= NL) d += P_[K - NL];  // + p R
-  d += st.cd;
-  s += st.cs;
+  uint64_t d = e + q + dm + st.cd;
+  s = s - e + q + sm + st.cs;
   if constexpr (K < NL) {
     st.md[K] = ((uint32_t)d * BGV_N0) & LMASK;
     st.ms[K] = ((uint32_t)s * BGV_N0) & LMASK;
@@ -138,13 +149,13 @@ BGV_HD void mul_col(mul_state& st, const uint32_t* a0, const uint32_t* a1, const
     r0[K - NL] = (uint32_t)d & LMASK;
     r1[K - NL] = (uint32_t)s & LMASK;
   }
-  st.cd = (uint64_t)((int64_t)d >> LBITS);
+  st.cd = d >> LBITS;
   st.cs = s >> LBITS;
 }
 template <int... K>
-BGV_HD void mul_cols(mul_state& st, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
+BGV_HD void mul_cols(mul_state& st, const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1n,
                      uint32_t* r0, uint32_t* r1, std::integer_sequence<int, K...>) {
-  (mul_col<K>(st, a0, a1, b0, b1, r0, r1), ...);
+  (mul_col<K>(st, a0, a1, b0, b1n, r0, r1), ...);
 }
 
 struct mul2_state {
@@ -189,19 +200,20 @@ BGV_HD void mul2_cols(mul2_state& st, const uint32_t* x, const uint32_t* y, cons
 }
 }  // namespace bgvw
 
-// r0 = REDC(a0 b0 - a1 b1) + p  in (0, 3p),  r1 = REDC((a0 + a1)(b0 + b1) - a0 b0 - a1 b1) in [0, 3p)
-// (operand values VA VB <= 2520); limbs 0..12 of each < 2^28, limb 13 the top carry.
+// r0 = REDC(a0 b0 + a1 (KM - b1)) = a0 b0 - a1 b1, r1 = REDC((a0 + a1)(b0 + b1) - a0 b0 + a1 (KM - b1))
+// = a0 b1 + a1 b0 (mod p); limbs 0..12 of each < 2^28, limb 13 the top carry.
 BGV_HD void fp2_mul_w_body(const uint32_t* a0, const uint32_t* a1, const uint32_t* b0, const uint32_t* b1,
                            uint32_t* r0, uint32_t* r1) {
-  const uint32_t P_[NL] = BGV_P_LIMBS;
   bgvw::mul_state st;
+  uint32_t b1n[NL];
   BGV_UNROLL for (int i = 0; i < NL; ++i) {
     st.sa[i] = a0[i] + a1[i];
     st.sb[i] = b0[i] + b1[i];
+    b1n[i] = bgvw::KM.v[i] - b1[i];
   }
   st.cd = st.cs = 0;
-  bgvw::mul_cols(st, a0, a1, b0, b1, r0, r1, std::make_integer_sequence<int, 2 * NL - 1>{});
-  r0[NL - 1] = (uint32_t)st.cd + P_[NL - 1];
+  bgvw::mul_cols(st, a0, a1, b0, b1n, r0, r1, std::make_integer_sequence<int, 2 * NL - 1>{});
+  r0[NL - 1] = (uint32_t)st.cd;
   r1[NL - 1] = (uint32_t)st.cs;
 }
 
@@ -215,6 +227,17 @@ BGV_HD void fp_mul2_w_body(const uint32_t* x, const uint32_t* y, const uint32_t*
   bgvw::mul2_cols(st, x, y, z, w, r0, r1, std::make_integer_sequence<int, 2 * NL - 1>{});
   r0[NL - 1] = (uint32_t)st.c0;
   r1[NL - 1] = (uint32_t)st.c1;
+}
+
+// (a0 + a1)(a0 - a1 + KS), (2 a0) a1 for limbs <= BGV_WSQR_LIMB, values < BGV_WSQR_V p
+BGV_HD void fp2_sqr_w_body(const uint32_t* a0, const uint32_t* a1, uint32_t* r0, uint32_t* r1) {
+  uint32_t x[NL], y[NL], z[NL];
+  BGV_UNROLL for (int i = 0; i < NL; ++i) {
+    x[i] = a0[i] + a1[i];
+    y[i] = a0[i] + (bgvw::KS.v[i] - a1[i]);
+    z[i] = a0[i] + a0[i];
+  }
+  fp_mul2_w_body(x, y, z, a1, r0, r1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -252,17 +275,12 @@ BGV_MUL_ATTR bgv_u28 fp2_mul_fp_w_l(BGV_U14(a0_), BGV_U14(a1_)) {
   return w28_pack(r0, r1);
 }
 
-// Fp2 square for operands with limbs <= BGV_WSQR_LIMB and values < BGV_WSQR_V p:
-// (a0 + a1)(a0 - a1 + k p), (2 a0) a1, no slot.  The k p is the redundant representation
-// bls_lazy.h builds for that bound (lzc::make_kp); the caller checks its bounds.
-#define BGV_WSQR_LIMB ((1ull << 28) + (1ull << 27))
-#define BGV_WSQR_V 8
-BGV_HD void fp2_sqr_w_body(const uint32_t* a0, const uint32_t* a1, const uint32_t* kp, uint32_t* r0, uint32_t* r1) {
-  uint32_t x[NL], y[NL], z[NL];
-  BGV_UNROLL for (int i = 0; i < NL; ++i) {
-    x[i] = a0[i] + a1[i];
-    y[i] = a0[i] + (kp[i] - a1[i]);
-    z[i] = a0[i] + a0[i];
-  }
-  fp_mul2_w_body(x, y, z, a1, r0, r1);
+// Fp2 square: no slot (operand bounds BGV_WSQR_LIMB / BGV_WSQR_V, checked by the caller)
+BGV_MUL_ATTR bgv_u28 fp2_sqr_w_l(BGV_U14(a0_), BGV_U14(a1_)) {
+  BGV_COUNT_SQR();
+  BGV_COUNT_SQR();
+  const uint32_t a0[NL] = {BGV_L14(a0_)}, a1[NL] = {BGV_L14(a1_)};
+  uint32_t r0[NL], r1[NL];
+  fp2_sqr_w_body(a0, a1, r0, r1);
+  return w28_pack(r0, r1);
 }

@@ -469,8 +469,8 @@ int hs_wide_check(int n, uint64_t seed) {
   bad += hs_wide_pair<LMASK, 2, LMASK, 2>(n);
   bad += hs_wide_pair<LMASK, 3, LMASK, 3>(n);
   bad += hs_wide_pair<(1u << 29) - 1, 4, (1u << 29) - 1, 4>(n);
-  bad += hs_wide_pair<(1u << 29) + (1u << 28), 6, LMASK, 3>(n);
-  bad += hs_wide_pair<LMASK, 20, LMASK, 30>(n);
+  bad += hs_wide_pair<(1u << 29) - 1, 40, LMASK, 8>(n);
+  bad += hs_wide_pair<LMASK, 8, (1u << 29) - 1, 8>(n);
   for (int t = 0; t < n + 3; ++t) {  // the squaring at its limb bound
     const int k = t < n ? 0 : t - n;
     const lz2<BGV_WSQR_LIMB, BGV_WSQR_V> a{hs_lz<BGV_WSQR_LIMB, BGV_WSQR_V>(k), hs_lz<BGV_WSQR_LIMB, BGV_WSQR_V>(k == 0 ? 0 : 2 - k / 2)};

@@ -186,10 +186,13 @@ def test_split_epoch_sweep_2p20(split_ctxs):
 # Retry placements in a bulk call (20,480 one-set jobs, more than BGV_LATENCY_MAX): single invalid
 # jobs at slots 0, 1, 37 and 63 of their groups, two and three in one group, an undecodable
 # signature beside an invalid job.  Round 4 ran these against an opt-in weighted test (slot k
-# with weight k + 1) and round 5 against the same test in the first pass; both measured equal or
-# slower at the headline (profiles/r04/weighted_ab/, profiles/r05/fpw_ab/) and are gone, so the
-# pattern tests decide.  Reference semantics: every job's verdict equals its own verification
-# (chain/bls/multithread/worker.ts:76-98 retry per job).
+# with weight k + 1) for every failing group and round 5 against the same test in the first
+# pass; both measured equal or slower at the headline (profiles/r04/weighted_ab/,
+# profiles/r05/fpw_ab/) and are gone.  The call's signing roots are all distinct, so it has no
+# uniform groups and the pattern tests decide here; the weighted test that remains (on by
+# default for failing uniform groups, BGV_WEIGHTED_UNIFORM) is covered by
+# test_gpu_r05.py::test_uniform_groups_weighted_positions.  Reference semantics: every job's
+# verdict equals its own verification (chain/bls/multithread/worker.ts:76-98 retry per job).
 # ---------------------------------------------------------------------------------------
 @pytest.fixture(scope="module")
 def weighted_ctx():

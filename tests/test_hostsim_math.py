@@ -466,7 +466,7 @@ def test_team_final_exp_check(L):
 def test_wide_fp2_products_equal_classic():
     """bls_wide.h's deferred-reduction Fp2 product, Fp2-by-Fp product and squaring (the bulk
     kernels' tower, blst mul_mont_384x style) against the fully reduced Karatsuba, mod p: random
-    operands at five bound pairs (normalized up to 2^29 + 2^28 limbs, values up to 30 p) and the
+    operands at five bound pairs (limbs up to 2^29, values up to 40 p) and the
     extreme ones (every limb at its bound, zero).  The host build also checks every lazy bound."""
     for variant in ("wide", "classic"):
         assert hs.lib(variant).hs_wide_check(400, 0xB15 + len(variant)) == 0
