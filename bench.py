@@ -72,6 +72,16 @@ def dist_env():
     return rank, world, local
 
 
+def node_devices(world: int, local: int):
+    """Devices of the single-process node-shape leg: every GPU of the node (one per rank) at
+    N > 1, the rank's own device twice at N = 1 (the two-device split rehearsed on one GPU), and
+    under the one-GPU rehearsal of N ranks (BGV_BENCH_DEVICE) that device N times -- so every
+    leg the N-GPU run takes also runs in the rehearsal, on the devices that exist."""
+    if "BGV_BENCH_DEVICE" in os.environ:
+        return [local] * max(world, 2)
+    return list(range(world)) if world > 1 else [local, local]
+
+
 def free_port() -> int:
     import socket
     with socket.socket() as sk:
@@ -834,7 +844,7 @@ def main():
     if args.node_shape == "on" or (args.node_shape == "auto" and world > 1):
         # rank 0 alone, while the other ranks wait at the barrier with their devices idle
         if rank == 0:
-            devs = list(range(world)) if world > 1 else [local, local]
+            devs = node_devices(world, local)
             shape = node_shape(native, devs, args.nkeys, 64, 16, args.settle_s, sweep=not args.no_epoch_sweep)
         barrier()
 

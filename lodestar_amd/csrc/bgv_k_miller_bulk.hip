@@ -35,6 +35,7 @@
 // as the products' per-lane LDS operand slot requires
 #ifndef BGV_LZ2_CLASSIC
 #define BGV_LZ2_WIDE 1
+#define BGV_LZ2_WIDE_STRICT 1  // no silent fallback to the fully reduced product
 #endif
 #include "bgv_device.h"
 

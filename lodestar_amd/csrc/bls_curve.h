@@ -127,7 +127,7 @@ BGV_HD jac_t<F> jac_add_raw(const jac_t<F>& p, const jac_t<F>& q, bool* h_zero, 
   const auto V = L_mulk<4>(L_mul(U1, HH));
   const auto X3 = L_norm(L_sub(L_sqr(rr), L_add(J, L_dbl(V))));
   const auto Y3 = L_sub(L_mul(rr, L_norm(L_sub(V, X3))), L_dbl(L_mul(S1, L_norm(J))));
-  const auto Z3 = L_mul(L_sub(L_sqr(L_norm(L_add(Z1, Z2))), L_add(Z1Z1, Z2Z2)), H);
+  const auto Z3 = L_mul(L_wnorm(L_sub(L_sqr(L_norm(L_add(Z1, Z2))), L_add(Z1Z1, Z2Z2))), H);
   jac_t<F> r;
   r.x = L_out(X3);
   r.y = L_out(Y3);

@@ -228,6 +228,10 @@ BGV_HD lz<LMASK, VA> lz_norm(const lz<LA, VA>& a) {
   static_assert(VA * (lzc::P13 + 1) <= LMASK, "lz_norm: top limb would exceed 28 bits");
   static_assert(LA + (1ull << 5) <= 0xffffffffull, "lz_norm: carry overflow");
   lz<LMASK, VA> r;
+  if constexpr (LA <= LMASK) {  // already normalized (a product, say): a copy
+    BGV_UNROLL for (int i = 0; i < NL; ++i) r.v[i] = a.v[i];
+    return r;
+  }
   uint32_t c = 0;
   BGV_UNROLL for (int i = 0; i < NL - 1; ++i) {
     const uint32_t s = a.v[i] + c;
@@ -414,6 +418,9 @@ constexpr int lz2_wide_side() {
 template <uint64_t LA, uint64_t VA, uint64_t LB, uint64_t VB>
 BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
   constexpr int side = lz2_wide_side<LA, VA, LB, VB>();
+#if defined(BGV_LZ2_WIDE_STRICT)
+  static_assert(side != 0, "lz2_mul: operands outside the deferred-reduction product's bounds");
+#endif
   if constexpr (side == 1)
     return lz2_mul_w(a, b);
   else if constexpr (side == 2)
@@ -423,6 +430,9 @@ BGV_HD auto lz2_mul(const lz2<LA, VA>& a, const lz2<LB, VB>& b) {
 }
 template <uint64_t LA, uint64_t VA>
 BGV_HD lz2r lz2_sqr(const lz2<LA, VA>& a) {
+#if defined(BGV_LZ2_WIDE_STRICT)
+  static_assert(LA <= BGV_WSQR_LIMB && VA <= BGV_WSQR_V, "lz2_sqr: operand outside the wide squaring's bounds");
+#endif
   if constexpr (LA <= BGV_WSQR_LIMB && VA <= BGV_WSQR_V)
     return lz2_sqr_w(a);
   else
@@ -449,6 +459,17 @@ BGV_HD lz2r lz2_mul_fp(const lz2<LA, VA>& a, const lz<LB, VB>& s) {
   return lz2_mul_fp_c(a, s);
 }
 #endif
+
+// An operand normalized for the deferred-reduction product only (its limb bounds are tighter
+// than the fully reduced product's): a no-op in the other units.
+template <uint64_t LA, uint64_t VA>
+BGV_HD auto lz2_wnorm(const lz2<LA, VA>& a) {
+#if defined(BGV_LZ2_WIDE)
+  return lz2_norm(a);
+#else
+  return a;
+#endif
+}
 
 // The eager fp2_t products of bls_field.h in a BGV_LZ2_WIDE unit (declared there): operand
 // components normalized (limbs < 2^28) with values < 8p, results weakly reduced (< 2p).
@@ -621,6 +642,9 @@ template <uint64_t A, uint64_t B> BGV_HD lzr L_red(const lz<A, B>& a) { return l
 template <uint64_t A, uint64_t B> BGV_HD lz2r L_red(const lz2<A, B>& a) { return lz2_red(a); }
 template <uint64_t A, uint64_t B> BGV_HD auto L_norm(const lz<A, B>& a) { return lz_norm(a); }
 template <uint64_t A, uint64_t B> BGV_HD auto L_norm(const lz2<A, B>& a) { return lz2_norm(a); }
+// an operand of a product normalized where the deferred-reduction Fp2 product needs it
+template <uint64_t A, uint64_t B> BGV_HD auto L_wnorm(const lz<A, B>& a) { return a; }
+template <uint64_t A, uint64_t B> BGV_HD auto L_wnorm(const lz2<A, B>& a) { return lz2_wnorm(a); }
 template <uint64_t A, uint64_t B, uint64_t C, uint64_t D>
 BGV_HD auto L_add(const lz<A, B>& a, const lz<C, D>& b) { return lz_add(a, b); }
 template <uint64_t A, uint64_t B, uint64_t C, uint64_t D>

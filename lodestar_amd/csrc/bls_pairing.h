@@ -179,7 +179,7 @@ BGV_MILLER_ATTR void lz_miller_dbl_lines(lz_tpt& t, const lz_mp& P, lz2r* l0, lz
   const auto X3 = lz2_sub(lz2_mulk<9>(lz2_sqr(A)), lz2_dbl(D));
   const auto Y3 = lz2_sub(lz2_mulk<3>(lz2_mul(A, lz2_norm(lz2_sub(D, X3)))), lz2_mulk<8>(C));
   const auto Z3 = lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.y, t.z))), lz2_add(B, ZZ));
-  *l3 = lz2_mul_fp(lz2_mul(Z3, ZZ), P.yp);
+  *l3 = lz2_mul_fp(lz2_mul(lz2_wnorm(Z3), ZZ), P.yp);
   t.x = lz2_red(X3);
   t.y = lz2_red(Y3);
   t.z = lz2_red(Z3);
@@ -216,7 +216,7 @@ BGV_MILLER_ATTR lzf12 lz_miller_add_step(const lzf12& f, lz_tpt& t, const lz_jq&
   const auto V = lz2_mulk<4>(lz2_mul(U1, HH));
   const auto X3 = lz2_norm(lz2_sub(lz2_sqr(r), lz2_add(J, lz2_dbl(V))));
   const auto Y3 = lz2_sub(lz2_mul(r, lz2_norm(lz2_sub(V, X3))), lz2_dbl(lz2_mul(S1, lz2_norm(J))));
-  const auto Z3 = lz2_mul(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, c.qz))), lz2_add(ZZ, c.zz)), H);
+  const auto Z3 = lz2_mul(lz2_wnorm(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, c.qz))), lz2_add(ZZ, c.zz))), H);
   const auto l0 = lz2_norm(lz2_sub(lz2_mul(r, c.xz), lz2_mul(c.y2z, Z3)));
   const lz2r l1 = lz2_red(lz2_mul(r, c.zzz_xn));
   const lz2r l3 = lz2_red(lz2_mul(Z3, c.zzz_yp));
@@ -292,7 +292,7 @@ BGV_MILLER_ATTR auto lz_pline_dbl(lz_tpt& t) {
   const auto X3 = lz2_sub(lz2_mulk<9>(lz2_sqr(A)), lz2_dbl(D));
   const auto Y3 = lz2_sub(lz2_mulk<3>(lz2_mul(A, lz2_norm(lz2_sub(D, X3)))), lz2_mulk<8>(C));
   const auto Z3 = lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.y, t.z))), lz2_add(B, ZZ));
-  const auto L3 = lz2_norm(lz2_mul(Z3, ZZ));
+  const auto L3 = lz2_norm(lz2_mul(lz2_wnorm(Z3), ZZ));
   t.x = lz2_red(X3);
   t.y = lz2_red(Y3);
   t.z = lz2_red(Z3);
@@ -317,7 +317,7 @@ BGV_MILLER_ATTR auto lz_pline_add(lz_tpt& t, const lz2r& qx, const lz2r& qy, con
   const auto V = lz2_mulk<4>(lz2_mul(U1, HH));
   const auto X3 = lz2_norm(lz2_sub(lz2_sqr(r), lz2_add(J, lz2_dbl(V))));
   const auto Y3 = lz2_sub(lz2_mul(r, lz2_norm(lz2_sub(V, X3))), lz2_dbl(lz2_mul(S1, lz2_norm(J))));
-  const auto Z3 = lz2_mul(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, qz))), lz2_add(ZZ, zz)), H);
+  const auto Z3 = lz2_mul(lz2_wnorm(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.z, qz))), lz2_add(ZZ, zz))), H);
   const auto L0 = lz2_norm(lz2_sub(lz2_mul(r, xz), lz2_mul(qy, Z3)));
   const auto L1 = lz2_norm(lz2_mul(r, zzz));
   const auto L3 = lz2_norm(lz2_mul(Z3, zzz));

@@ -36,3 +36,19 @@ def test_rank_count_mismatch_fails_loudly():
     r = _run(["--gpus", "2", "--check-ranks"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "--gpus 2 but 1 rank(s)" in (r.stderr + r.stdout)
+
+
+def test_node_shape_devices(monkeypatch):
+    """The node-shape leg's devices (bench.node_devices): every GPU at N > 1; under the one-GPU
+    rehearsal (BGV_BENCH_DEVICE) the rehearsal's device once per rank, so `BGV_BENCH_DEVICE=0
+    bench.py --gpus 2` runs the leg on devices that exist."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("BGV_BENCH_DEVICE", raising=False)
+    assert bench.node_devices(8, 3) == list(range(8))
+    assert bench.node_devices(2, 1) == [0, 1]
+    assert bench.node_devices(1, 0) == [0, 0]
+    monkeypatch.setenv("BGV_BENCH_DEVICE", "0")
+    assert bench.node_devices(2, 0) == [0, 0]
+    assert bench.node_devices(4, 0) == [0, 0, 0, 0]
+    assert bench.node_devices(1, 0) == [0, 0]

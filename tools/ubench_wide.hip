@@ -62,7 +62,26 @@ __host__ __device__ inline uint32_t fold12(const lzf12u& f) {
 // the chains, one per lane
 template <int OP>
 __host__ __device__ inline uint32_t chain(uint32_t seed, uint32_t tid, int iters) {
-  if constexpr (OP == 0 || OP == 1) {
+  if constexpr (OP == 4 || OP == 5) {
+    // the deferred-reduction body inlined (no call, no slot): the call and LDS overhead of OP 0;
+    // OP 5 also without the result's reduction to the fp_t invariant
+    lz2r x = seed_fp2(seed, tid);
+    const lz2r y = seed_fp2(seed + 7, tid);
+    for (int k = 0; k < iters; ++k) {
+      uint32_t r0[NL], r1[NL];
+      fp2_mul_w_body(x.c0.v, x.c1.v, y.c0.v, y.c1.v, r0, r1);
+      lz2<LMASK, 2> o;
+      for (int i = 0; i < NL; ++i) {
+        o.c0.v[i] = r0[i];
+        o.c1.v[i] = r1[i];
+      }
+      if constexpr (OP == 4)
+        x = lz2_red(o);
+      else
+        x = o;
+    }
+    return fold(x);
+  } else if constexpr (OP == 0 || OP == 1) {
     lz2r x = seed_fp2(seed, tid);
     const lz2r y = seed_fp2(seed + 7, tid);
     for (int k = 0; k < iters; ++k) {
@@ -92,12 +111,12 @@ k_chain(uint32_t* out, uint32_t seed, int iters) {
   out[tid] = chain<OP>(seed, tid, iters);
 }
 
-static const char* kOpName[4] = {"fp2_mul", "fp2_sqr", "fp12_sqr", "mul_line"};
+static const char* kOpName[6] = {"fp2_mul", "fp2_sqr", "fp12_sqr", "mul_line", "fp2_mul_inline", "fp2_mul_body_only"};
 
 template <int OP, int WPS>
 static int run(uint32_t* d, int cus) {
   const int blocks = cus * 4 * WPS;
-  const int iters = OP < 2 ? 4096 : 256;
+  const int iters = (OP < 2 || OP >= 4) ? 4096 : 256;
   const int n = blocks * 64;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -136,6 +155,8 @@ int main() {
   CHECK(hipMalloc(&d, sizeof(uint32_t) * cus * 4 * 2 * 64));
   int bad = 0;
   bad += run<0, 1>(d, cus);
+  bad += run<4, 1>(d, cus);
+  bad += run<5, 1>(d, cus);
   bad += run<1, 1>(d, cus);
   bad += run<2, 1>(d, cus);
   bad += run<3, 1>(d, cus);
