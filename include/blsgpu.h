@@ -189,6 +189,20 @@ int bgv_final_verify(bgv_ctx* ctx, const uint8_t* partials, size_t n, int32_t* o
 int bgv_debug_prepare(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, int path, uint64_t seed, uint8_t* out_h192,
                       uint8_t* out_f576, int32_t* out_status);
 
+/* Parity hook for uniform groups (tests only; bgv_api.cpp call_submit / call_build_parts).
+ * The n sets (2..64, cached pubkeys, one signing root, 96-B signatures) form ONE uniform
+ * first-pass group of a bulk batch, randomizers as bgv_debug_prepare's; then ntests retry tests
+ * over its slots, each a slot mask (bit k = set k), weighted (slot k with weight k + 1,
+ * BGV_GROUP_WEIGHTED) when test_weighted[t] != 0.  Replaces the per-set pairs of a group whose
+ * sets share a root, prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H):
+ *   out_first576       MillerLoop(sum_i r_i pk_i, H)                (k_gsum -> k_lines / k_facc)
+ *   out_pk576[t]       MillerLoop(sum_{i in t} w_i r_i pk_i, H)     (k_gsum / k_gsum_w -> k_miller_team)
+ *   out_sig576[t]      MillerLoop(-G1, sum_{i in t} w_i r_i sig_i)  (the test's signature pair)
+ * 576-byte values as bgv_debug_prepare's f; w_i = 1, or i + 1 in a weighted test. */
+int bgv_debug_uniform(bgv_ctx* ctx, const bgv_set* sets, size_t nsets, uint64_t seed, const uint64_t* test_masks,
+                      const uint32_t* test_weighted, size_t ntests, uint8_t* out_first576, uint8_t* out_pk576,
+                      uint8_t* out_sig576);
+
 /* SURVEY 8(f) rows beside the verify path -------------------------------- */
 
 /* Deposit-time pubkey validation: bls.PublicKey.fromBytes(pubkey, CoordType.affine,

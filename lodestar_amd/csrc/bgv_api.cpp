@@ -1111,8 +1111,13 @@ static void call_build_parts(Call* call, std::vector<bgv_dgroup>& rg, int64_t gb
       // a failing uniform group almost always holds ONE invalid slot (a wrong key): one test with
       // slot k weighted by k + 1 names it (BGV_GROUP_WEIGHTED; k_final12 finds w with V^w = W)
       // instead of ~6 pattern tests of two Miller loops each; otherwise the pattern tests follow
-      // (unit_rounds -1).  Two or more invalid slots match some w <= 64 only with negligible
-      // probability (their values are independent elements of prime order r).
+      // (unit_rounds -1).  Soundness with two or more invalid slots: write slot k's pairing
+      // defect as g^(e_k) in the prime-order group GT (e_k != 0 for an invalid slot; the
+      // signatures, hence the e_k, are the attacker's, fixed before the secret randomizers are
+      // drawn).  V^w = W means sum_k (k + 1 - w) r_k e_k = 0 (mod r), a linear equation in the
+      // secret r_k with a nonzero coefficient on at least one of them; r_k takes 2^64 distinct
+      // values mod r, so for one w it holds with probability <= 2^-64, and over the 64 candidate
+      // w with <= 64 * 2^-64 per failing group (a match would accept the other invalid jobs).
       PatternUnit pu;
       pu.group = (uint32_t)ug;
       pu.kind = 2;
@@ -2538,6 +2543,117 @@ int bgv_debug_prepare(bgv_ctx* c, const bgv_set* sets, size_t nsets, int path, u
     out_status[2 * i + 1] = ps[i];
   }
   return BGV_OK;
+}
+
+int bgv_debug_uniform(bgv_ctx* c, const bgv_set* sets, size_t nsets, uint64_t seed, const uint64_t* test_masks,
+                      const uint32_t* test_weighted, size_t ntests, uint8_t* out_first576, uint8_t* out_pk576,
+                      uint8_t* out_sig576) {
+  if (!c || nsets < 2 || nsets > BGV_WAVE || !sets || !out_first576 || ntests > BGV_WAVE ||
+      (ntests && (!test_masks || !test_weighted || !out_pk576 || !out_sig576)))
+    return -BGV_E_ARG;
+  std::shared_lock<std::shared_mutex> clk(c->cache_mu);
+  if (c->closed) return -BGV_E_CLOSED;
+  // one uniform first-pass group: every set signs the first set's root (hsrc 0)
+  std::vector<bgv_dslot> slots;
+  std::vector<uint32_t> idx;
+  uint64_t state = seed;
+  uint32_t max_npk = 0;
+  for (size_t i = 0; i < nsets; ++i) {
+    const bgv_set& st = sets[i];
+    if (!st.pk_indices || st.n_pk == 0 || !st.msg || st.sig_len != 96 || !st.sig ||
+        memcmp(st.msg, sets[0].msg, 32) != 0)
+      return -BGV_E_ARG;
+    for (uint32_t q = 0; q < st.n_pk; ++q)
+      if (st.pk_indices[q] >= c->n_pubkeys || c->bad_pk.count(st.pk_indices[q])) return -BGV_E_BAD_INDEX;
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.flags = BGV_SLOT_PK_CACHED;
+    s.n_pk = st.n_pk;
+    s.sig_len = st.sig_len;
+    s.pk_off = (uint32_t)idx.size();
+    idx.insert(idx.end(), st.pk_indices, st.pk_indices + st.n_pk);
+    memcpy(s.msg, st.msg, 32);
+    memcpy(s.sig, st.sig, 96);
+    s.group = 0;
+    s.hsrc = 0;
+    do s.scalar = splitmix64(&state);
+    while (s.scalar == 0);
+    max_npk = std::max(max_npk, st.n_pk);
+    slots.push_back(s);
+  }
+  while (slots.size() % BGV_WAVE) {
+    bgv_dslot s;
+    memset(&s, 0, sizeof(s));
+    s.flags = BGV_SLOT_PAD;
+    s.hsrc = (uint32_t)slots.size();
+    slots.push_back(s);
+  }
+  const uint32_t nslots = (uint32_t)slots.size(), nt = (uint32_t)ntests;
+  const bgv_dgroup first{0u, (uint32_t)nsets, BGV_ALL_SLOTS, 0u, BGV_GROUP_UNIFORM};
+  // the tests as a retry round lays them out (retry_launch): groups, then the uniform list
+  const uint32_t per = (uint32_t)(sizeof(bgv_dgroup) / sizeof(uint32_t));
+  const uint32_t nlist = (nt + per - 1) / per;
+  std::vector<bgv_dgroup> tg(nt + nlist);
+  bool weighted = false;
+  for (uint32_t t = 0; t < nt; ++t) {
+    tg[t] = bgv_dgroup{0u, (uint32_t)nsets, test_masks[t], 0u,
+                       BGV_GROUP_UNIFORM | (test_weighted[t] ? BGV_GROUP_WEIGHTED : 0u)};
+    weighted = weighted || test_weighted[t];
+    reinterpret_cast<uint32_t*>(tg.data() + nt)[t] = t;
+  }
+  std::lock_guard<std::mutex> lk(c->util_mu);
+  Device& d = c->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  Exec* x = new Exec();
+  uint8_t* dout = nullptr;
+  int rc = exec_create(x);
+  hipStream_t dstream = nullptr;
+  if (!rc && hipStreamCreateWithFlags(&dstream, hipStreamNonBlocking) != hipSuccess) rc = -BGV_E_DEVICE;
+  x->main = dstream;
+  if (!rc) rc = exec_reserve_slots(*x, nslots);
+  if (!rc) rc = exec_reserve_groups(*x, std::max<uint32_t>(1, nt + nlist));
+  if (!rc) rc = grow(&x->d_idx, &x->idx_cap, idx.size());
+  if (!rc && hipMalloc(reinterpret_cast<void**>(&dout), 576ull * (1 + 2 * nt)) != hipSuccess) rc = -BGV_E_DEVICE;
+  if (!rc) {
+    bgv_dev_batch b = make_batch(d, *x, nslots, 1);
+    b.max_npk = max_npk;
+    b.path = BGV_PATH_BULK;
+    b.uniform = true;
+    rc = exec_reserve_lines(*x, b);
+    bgv_streams S{x->main, nullptr};
+    bool ok = rc == BGV_OK &&
+        hipMemcpyAsync(x->d_slots, slots.data(), sizeof(bgv_dslot) * nslots, hipMemcpyHostToDevice, x->main) ==
+            hipSuccess &&
+        hipMemcpyAsync(x->d_groups, &first, sizeof(bgv_dgroup), hipMemcpyHostToDevice, x->main) == hipSuccess &&
+        hipMemcpyAsync(x->d_idx, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice, x->main) == hipSuccess &&
+        bgv_launch_sets(b, S) == hipSuccess &&
+        bgv_launch_fp12_bytes(b.gpkp, 1, dout, x->main) == hipSuccess;
+    if (ok && nt) {
+      // the tests over the first pass's per-slot results (r_i sig_i, r_i pk_i, H)
+      bgv_dev_batch t = make_batch(d, *x, nslots, nt);
+      t.max_npk = max_npk;
+      t.path = BGV_PATH_BULK;
+      t.uniform = true;
+      t.upk = reinterpret_cast<const uint32_t*>(t.groups + nt);
+      t.npk = nt;
+      t.weighted = weighted;
+      ok = hipMemcpyAsync(x->d_groups, tg.data(), sizeof(bgv_dgroup) * tg.size(), hipMemcpyHostToDevice, x->main) ==
+               hipSuccess &&
+           bgv_launch_gpairs(t, x->main) == hipSuccess &&
+           bgv_launch_fp12_bytes(t.gpkp, nt, dout + 576, x->main) == hipSuccess &&
+           bgv_launch_fp12_bytes(t.gpair, nt, dout + 576ull * (1 + nt), x->main) == hipSuccess &&
+           hipMemcpyAsync(out_pk576, dout + 576, 576ull * nt, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+           hipMemcpyAsync(out_sig576, dout + 576ull * (1 + nt), 576ull * nt, hipMemcpyDeviceToHost, x->main) ==
+               hipSuccess;
+    }
+    ok = ok && hipMemcpyAsync(out_first576, dout, 576, hipMemcpyDeviceToHost, x->main) == hipSuccess &&
+         hipStreamSynchronize(x->main) == hipSuccess;
+    if (!ok) rc = -BGV_E_DEVICE;
+  }
+  if (dout) (void)hipFree(dout);
+  exec_destroy(x);
+  if (dstream) (void)hipStreamDestroy(dstream);
+  return rc;
 }
 
 int bgv_aggregate_pubkeys(bgv_ctx* c, const uint32_t* idx, size_t n, uint8_t out96[96]) {

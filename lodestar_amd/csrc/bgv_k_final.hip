@@ -287,6 +287,18 @@ __global__ void k_fp12_to_bytes(const fp12_t* __restrict__ in, uint8_t* __restri
   }
 }
 
+// n values -> 576 canonical bytes each (one lane per value; parity hooks)
+__global__ void k_fp12_n_to_bytes(const fp12_t* __restrict__ in, uint32_t n, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const fp_t* v = reinterpret_cast<const fp_t*>(in + i);
+  for (int k = 0; k < 12; ++k) {
+    uint8_t b[48];
+    fp_to_be48(b, fp_from_mont(v[k]));
+    for (int q = 0; q < 48; ++q) out[576ull * i + 48 * k + q] = b[q];
+  }
+}
+
 // n serialized values -> Montgomery Fp12; status[i] = 0, or BGV_BAD_ENCODING for a
 // coefficient >= p.  one[0] receives 1 (the group pair slot of a k_final over the values).
 __global__ void k_fp12_from_bytes(const uint8_t* __restrict__ in, uint32_t n, fp12_t* __restrict__ out,
@@ -358,6 +370,11 @@ hipError_t bgv_launch_partial(const bgv_dev_batch& b, uint32_t g0, uint32_t ng, 
   return hipGetLastError();
 }
 size_t bgv_fp12_bytes() { return sizeof(fp12_t); }
+hipError_t bgv_launch_fp12_bytes(const fp12_t* in, uint32_t n, uint8_t* out576, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_n_to_bytes, dim3(nblk(n, 64)), dim3(64), 0, st, in, n, out576);
+  return hipGetLastError();
+}
 
 // prod of n serialized partials, then the final-exponentiation check (one k_final group)
 hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, void* one, const bgv_dgroup* group,

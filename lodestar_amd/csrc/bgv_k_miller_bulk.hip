@@ -130,6 +130,26 @@ __global__ void BGV_KATTR_FACC k_facc(const bgv_dslot* __restrict__ slots, uint3
     *out = fp12_one();
     return;
   }
+#if BGV_WPE_FACC >= 2
+  // Two waves per SIMD (A/B: BGV_WPE_FACC=2): 8 waves per CU leave 20 KB of LDS each, so no
+  // staging -- the records are read straight into registers (the other wave hides the loads)
+  // and P's constants stay in registers; the LDS holds only the products' operand slot.
+  {
+    const uint32_t* base = lines + 4 * (size_t)lp;
+    const miller_p P0 = miller_p_make(*P);
+    *out = miller_facc_walk_staged([&](int k, uint32_t z, auto* r) {
+      const uint4* src = reinterpret_cast<const uint4*>(base + (size_t)(k + z) * BGV_LINE_QUADS * 4 * cap);
+      uint4* w = reinterpret_cast<uint4*>(r);
+      BGV_UNROLL for (int d = 0; d < BGV_LINE_QUADS; ++d) w[d] = src[(size_t)d * cap];
+    }, [&](int which, uint32_t z) {
+      const fp_t& c = which == 0 ? P0.xn : (which == 1 ? P0.yp : P0.zp3);
+      lzr v;
+      BGV_UNROLL for (int i = 0; i < NL; ++i) v.v[i] = c.v[i] + z;
+      return v;
+    });
+    return;
+  }
+#endif
   // this wave's LDS: the staged record [quad][lane] and P's constants [word][lane]
   __shared__ uint4 rec_lds[BGV_LINE_QUADS][64];
   __shared__ uint32_t p_lds[3 * NL][64];

@@ -122,6 +122,7 @@ hipError_t bgv_launch_sig_aggregate(const uint8_t* sigs96, const uint32_t* lens,
                                     uint8_t* out96, hipStream_t st);
 size_t bgv_g2_point_bytes();
 size_t bgv_fp12_bytes();
+hipError_t bgv_launch_fp12_bytes(const fp12_t* in, uint32_t n, uint8_t* out576, hipStream_t st);  // parity hooks
 hipError_t bgv_launch_partial(const bgv_dev_batch& b, uint32_t g0, uint32_t ng, void* scratch, uint8_t* out576,
                               hipStream_t st);
 hipError_t bgv_launch_final_verify(const uint8_t* in, uint32_t n, void* vals, void* one, const bgv_dgroup* group,

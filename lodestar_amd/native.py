@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "bgv_verify_async", "bgv_aggregate_pubkeys", "bgv_hash_to_g2", "bgv_keygen", "bgv_sign",
     "bgv_set_rng_seed", "bgv_strerror", "bgv_device_count", "bgv_profile",
     "bgv_pubkeys_validate", "bgv_aggregate_signatures", "bgv_deposits_verify", "bgv_set_batching",
-    "bgv_verify_partial", "bgv_final_verify", "bgv_debug_prepare", "bgv_set_split",
+    "bgv_verify_partial", "bgv_final_verify", "bgv_debug_prepare", "bgv_debug_uniform", "bgv_set_split",
 ]
 
 
@@ -107,6 +107,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_verify_partial": ([P, P, SZ, P, P], ctypes.c_int),
             "bgv_final_verify": ([P, P, SZ, P], ctypes.c_int),
             "bgv_debug_prepare": ([P, P, SZ, ctypes.c_int, U64, P, P, P], ctypes.c_int),
+            "bgv_debug_uniform": ([P, P, SZ, U64, P, P, SZ, P, P, P], ctypes.c_int),
             "bgv_strerror": ([ctypes.c_int], ctypes.c_char_p),
             "bgv_device_count": ([], ctypes.c_int),
             "bgv_profile": ([P, ctypes.c_int, P, P, ctypes.c_int, P], ctypes.c_int),
@@ -115,7 +116,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "bgv_deposits_verify": ([P, P, P, P, SZ, P], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
-            if name in ("bgv_debug_prepare", "bgv_set_split") and path != os.path.join(HERE, "libblsgpu.so") and \
+            if name in ("bgv_debug_prepare", "bgv_debug_uniform", "bgv_set_split") and path != os.path.join(HERE, "libblsgpu.so") and \
                     not hasattr(lib, name):
                 continue  # parity hook absent from an older A/B build (tools/gpu/ab.sh)
             fn = getattr(lib, name)
@@ -307,6 +308,20 @@ class Context:
         _check(self.lib.bgv_debug_prepare(self._h, packed.sets, n, path, seed, h, f, st))
         return [(h.raw[192 * i:192 * i + 192], f.raw[576 * i:576 * i + 576], st[2 * i], st[2 * i + 1])
                 for i in range(n)]
+
+    def debug_uniform(self, sets, seed: int, tests=()):
+        """bgv_debug_uniform (parity hook): one uniform group of the sets (one signing root) and
+        retry tests over it, tests = [(slot mask, weighted)].  Returns (MillerLoop(sum r_i pk_i, H),
+        [(test's pubkey-sum pair, test's signature pair)]), 576 B each."""
+        packed = PackedCall([(list(sets), False)])
+        n, nt = packed.nsets, len(tests)
+        masks = (ctypes.c_uint64 * max(1, nt))(*[m for m, _ in tests])
+        wts = (ctypes.c_uint32 * max(1, nt))(*[1 if w else 0 for _, w in tests])
+        first = ctypes.create_string_buffer(576)
+        pk = ctypes.create_string_buffer(576 * max(1, nt))
+        sig = ctypes.create_string_buffer(576 * max(1, nt))
+        _check(self.lib.bgv_debug_uniform(self._h, packed.sets, n, seed, masks, wts, nt, first, pk, sig))
+        return first.raw, [(pk.raw[576 * t:576 * t + 576], sig.raw[576 * t:576 * t + 576]) for t in range(nt)]
 
     def final_verify(self, partials: Sequence[bytes]) -> bool:
         """Product of serialized partials and one final exponentiation == 1 (bgv_final_verify)."""

@@ -49,3 +49,55 @@ def test_uniform_retry_just_above_latency_bound(ctx, n):
     got = c.verify_jobs(jobs, native.MODE_WORKER, stats=st)
     assert got == want
     assert st.batch_retries >= 4
+
+
+# ---------------------------------------------------------------------------------------
+# Uniform groups pinned by value (VERDICT r05 "next" #2).  A group whose sets share one root
+# takes ONE Miller loop over its pubkey sum, prod_i e(r_i pk_i, H) = e(sum_i r_i pk_i, H); its
+# retry tests pair their own pubkey sums, and the weighted test weights slot k by k + 1.
+# bgv_debug_uniform injects the randomizers (the i-th nonzero splitmix64 word of the seed,
+# r = lo + hi x^2 mod r, as bgv_debug_prepare) and returns those Miller values; each is final-
+# exponentiated here with the oracle's final exponentiation and compared with the oracle's
+# pairing value.  With sig_i = sk_i H and pk_i = sk_i G1 every expected value is a power of
+# gt = e(G1, H):  e(sum w_i r_i pk_i, H) = gt^a and e(-G1, sum w_i r_i sig_i) = gt^-a with
+# a = sum w_i r_i sk_i (mod r).  Bit-exact integer work; reference:
+# packages/beacon-node/src/chain/bls/maybeBatch.ts:18-25, multithread/worker.ts:76-98.
+# ---------------------------------------------------------------------------------------
+def test_uniform_group_values_pinned_to_oracle():
+    import json
+    import os
+    from lodestar_amd import native
+    from oracle import bls12381 as o
+    from tests.test_pairing_golden import f12_from_bytes
+    from tools.gen_golden_r04 import randomizers
+    here = os.path.dirname(os.path.abspath(__file__))
+    keys = json.load(open(os.path.join(here, "golden", "keys.json")))
+    n = 40
+    sks = [int(v, 16) for v in keys["sk"][:n]]
+    c = native.Context([0])
+    try:
+        c.pubkeys_put(0, b"".join(bytes.fromhex(k) for k in keys["pk_compressed"][:n]), native.PK_COMPRESSED)
+        msg = hashlib.sha256(b"r06-uniform-values").digest()
+        sigs = c.sign(b"".join(sk.to_bytes(32, "big") for sk in sks), msg * n)
+        sets = [native.SetSpec(msg, sigs[96 * i:96 * i + 96], pk_indices=[i]) for i in range(n)]
+        seed = 0x5EED0006
+        rs = [r for _, r in randomizers(seed, n)]
+        wrong_slot = 23  # the weighted test names one slot; its weight is 24
+        tests = [(sum(1 << k for k in range(n) if k & 1), False),          # a pattern test S_0
+                 (sum(1 << k for k in range(n) if k & 4), False),          # S_2
+                 ((1 << n) - 1, True),                                     # the weighted test
+                 (((1 << n) - 1) & ~(1 << wrong_slot), True)]              # weighted, one slot dead
+        first, vals = c.debug_uniform(sets, seed, tests)
+    finally:
+        c.close()
+    gt = o.pairing(o.G1, o.hash_to_g2(msg))
+
+    def expect(mask, weighted):
+        a = sum(((k + 1) if weighted else 1) * rs[k] * sks[k] for k in range(n) if (mask >> k) & 1) % o.R
+        return o.f12_pow(gt, a)
+
+    assert o.final_exp(f12_from_bytes(first)) == expect((1 << n) - 1, False)
+    for (mask, weighted), (pk576, sig576) in zip(tests, vals):
+        e = expect(mask, weighted)
+        assert o.final_exp(f12_from_bytes(pk576)) == e, (hex(mask), weighted, "pubkey-sum pair")
+        assert o.final_exp(f12_from_bytes(sig576)) == o.f12_inv(e), (hex(mask), weighted, "signature pair")
