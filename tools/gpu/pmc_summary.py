@@ -23,8 +23,8 @@ for path in glob.glob(os.path.join(root, "**", "*counter_collection*.csv"), recu
                                 "agpr": row.get("Accum_VGPR_Count"), "scratch": row.get("Scratch_Size")})
     for (k, _, c), v in per_dispatch.items():
         acc[k][c].append(v)
-out = {"note": "rocprofv3 --pmc, one counter group per run (tools/gpu/pmc.sh), one unloaded 131072-set verify "
-               "call; values averaged per dispatch",
+out = {"note": "rocprofv3 --pmc, one counter group per run (tools/gpu/pmc.sh), one unloaded 64512-set verify "
+               "call (tools/gpu/roof_call.py); values averaged per dispatch",
        "per_dispatch": {k: {c: sum(v) / len(v) for c, v in sorted(cs.items())} for k, cs in sorted(acc.items())},
        "kernel_meta": meta}
 d = out["per_dispatch"]
