@@ -4,6 +4,7 @@
 #include "bgv_device.h"
 
 #include "bgv_team_dev.h"
+#include "bgv_rns.h"
 
 
 // A group's verdict bits from its u (bls_team.h tm_final_exp_u; pairing value conj(u)/u):
@@ -169,8 +170,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 // chain; 8 teams measured 0.86 ms for the 64-set gossip call).  The final exponentiation then runs on the
 // whole block with each coefficient's products split over eight lanes (tm_wide_ops_t<false, 8>):
 // one double-width product per lane for a squaring (two for a product) instead of 7 on one.
-// LEAN: the squarings with the lane's operand recipes (bgv_team_dev.h tm_wide8_lean_ops; the
-// same parts bit for bit); BGV_FOLD_LEAN=0 selects the select-based forms for an A/B.
+// ENGINE 2 (round 6, the default k_final_fold): the final exponentiation in residue arithmetic
+// (bgv_rns.h) on a 384-thread block, one residue of one coefficient per lane and one Montgomery
+// reduction (two base extensions) per coefficient and operation: 0.96 against 1.89 us per Fp12
+// operation of the eight-part engine (tools/ubench_rns.hip, profiles/r06/rns/); the fold keeps
+// its 16 teams, the block's other 128 threads (teams 16..23) run the same products on ones so
+// every thread reaches every barrier.  ENGINE 1 (k_final_fold_p8, BGV_FOLD_RNS=0): the
+// eight-part engine with the lane's squaring recipes (bgv_team_dev.h tm_wide8_lean_ops);
+// ENGINE 0 (k_final_fold_sel, BGV_FOLD_RNS=0 BGV_FOLD_LEAN=0) its select-based forms.  The same
+// field elements every way: u, the verdict bits and gu agree.
 }  // extern "C"
 template <bool LEAN>
 __device__ auto bgv_fold_ops_pick() {
@@ -180,19 +188,23 @@ __device__ auto bgv_fold_ops_pick() {
     return tm_wide_ops_t<false, 8>{};
 }
 #ifndef BGV_FOLD_TEAMS
-#define BGV_FOLD_TEAMS 16  // 16-lane teams of k_final_fold's block (BGV_FOLD_THREADS threads)
+#define BGV_FOLD_TEAMS 16  // 16-lane teams of k_final_fold's fold (BGV_FOLD_THREADS threads)
 #endif
 #define BGV_FOLD_THREADS (BGV_FOLD_TEAMS * BGV_TEAM)
-template <bool LEAN>
+#define BGV_FOLD_RNS_THREADS BGV_RNS_THREADS
+static_assert(BGV_FOLD_RNS_THREADS % BGV_TEAM == 0 && BGV_FOLD_RNS_THREADS >= BGV_FOLD_THREADS, "fold block");
+template <int ENGINE>
 __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ groups, uint32_t ngroups,
                                                 const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                                 int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
                                                 fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
                                                 const fp12_t* __restrict__ fsig) {
-  __shared__ fp_t lds[BGV_FOLD_TEAMS][2 * BGV_TEAM_COMPS];
+  constexpr int kTeams = (ENGINE == 2 ? BGV_FOLD_RNS_THREADS : BGV_FOLD_THREADS) / BGV_TEAM;
+  __shared__ fp_t lds[kTeams][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FOLD_TEAMS][BGV_TEAM_COMPS];
   __shared__ fp_t W[BGV_TEAM_COMPS], WA[BGV_TEAM_COMPS], WB[BGV_TEAM_COMPS], WP[8 * BGV_TEAM_COMPS];
   const int team = threadIdx.x / BGV_TEAM, c = threadIdx.x % BGV_TEAM;
+  const bool fold = team < BGV_FOLD_TEAMS;  // teams past the fold's 16 multiply ones
   const int cc = c < BGV_TEAM_COMPS ? c : c - 4;
   const uint32_t gi = blockIdx.x;
   const bgv_dgroup g = groups[gi < ngroups ? gi : ngroups - 1];
@@ -207,7 +219,7 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
   const uint32_t nmax = (g.n_slots + BGV_FOLD_TEAMS - 1) / BGV_FOLD_TEAMS;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
     const uint32_t idx = team + BGV_FOLD_TEAMS * k;
-    const bool in = grp_has(g, idx);
+    const bool in = fold && grp_has(g, idx);
     const fp_t y = in ? fs[kFp12 * idx + fi] : one_c;
     x = o.mul(x, y);
     if (ss) x = o.mul(x, in ? ss[kFp12 * idx + fi] : one_c);  // grid-uniform branch
@@ -215,7 +227,7 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
   // the eight partial products as a tree: every team multiplies at every level (the barriers
   // inside o.mul), team t keeps parts 2t and 2t + 1 of the level
   BGV_UNROLL for (int w = BGV_FOLD_TEAMS; w > 1; w >>= 1) {
-    if (c < BGV_TEAM_COMPS) part[team][cc] = x;
+    if (fold && c < BGV_TEAM_COMPS) part[team][cc] = x;
     __syncthreads();
     const int t2 = 2 * (team % (w >> 1));
     x = o.mul(part[t2][cc], part[t2 + 1][cc]);
@@ -224,32 +236,55 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
   // the final exponentiation on the whole block with the wide products (bgv_team_dev.h)
   if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
   __syncthreads();
-  const int wc = threadIdx.x % BGV_TEAM_COMPS, wq = threadIdx.x / BGV_TEAM_COMPS;
-  using OW = decltype(bgv_fold_ops_pick<LEAN>());
-  OW ow;
-  ow.A = WA;
-  ow.B = WB;
-  ow.P = WP;
-  ow.c = wc;
-  ow.q = wq;
-  if constexpr (LEAN) tm_sqr_rec8(wc, wq, &ow.rx, &ow.ry);
-  const fp_t xw = W[wc];
-  const int wfi = tm_fp_index(wc);
-  const fp_t u = tm_final_exp_u(ow, xw);
-  if (gu && gi < ngroups && wq == 0) reinterpret_cast<fp_t*>(gu + gi)[wfi] = u;
-  const int32_t v = verdict_bits(ow, u, g, gu1, wfi);
-  if (gi < ngroups && threadIdx.x == 0) verdict[gi] = v;
+  if constexpr (ENGINE == 2) {
+    // residue arithmetic (bgv_rns.h): W in, u (and gu, the verdict bits) out; every branch
+    // below is uniform over the block (gu, gu1 over the grid, g.ref1 over the block)
+    __shared__ rns_smem RS;
+    rns_ops ro;
+    ro.init(&RS, threadIdx.x);
+    const uint32_t u = tm_final_exp_u(ro, ro.from_fp(W[ro.c]));
+    const int rfi = tm_fp_index(ro.c);
+    if (gu && gi < ngroups) {
+      const fp_t uf = ro.to_fp(u);
+      if (ro.i == 0) reinterpret_cast<fp_t*>(gu + gi)[rfi] = uf;
+    }
+    int32_t v = ro.is_fp6(u) ? 1 : 0;
+    if (gu1 && g.ref1) {  // see verdict_bits
+      const uint32_t ur = ro.from_fp(reinterpret_cast<const fp_t*>(gu1 + (g.ref1 - 1))[rfi]);
+      if (ro.is_fp6(ro.mul(ur, ro.conj(u)))) v |= 2;
+    }
+    if (gi < ngroups && threadIdx.x == 0) verdict[gi] = v;
+  } else {
+    const int wc = threadIdx.x % BGV_TEAM_COMPS, wq = threadIdx.x / BGV_TEAM_COMPS;
+    using OW = decltype(bgv_fold_ops_pick<ENGINE == 1>());
+    OW ow;
+    ow.A = WA;
+    ow.B = WB;
+    ow.P = WP;
+    ow.c = wc;
+    ow.q = wq;
+    if constexpr (ENGINE == 1) tm_sqr_rec8(wc, wq, &ow.rx, &ow.ry);
+    const fp_t xw = W[wc];
+    const int wfi = tm_fp_index(wc);
+    const fp_t u = tm_final_exp_u(ow, xw);
+    if (gu && gi < ngroups && wq == 0) reinterpret_cast<fp_t*>(gu + gi)[wfi] = u;
+    const int32_t v = verdict_bits(ow, u, g, gu1, wfi);
+    if (gi < ngroups && threadIdx.x == 0) verdict[gi] = v;
+  }
 }
 extern "C" {
 #define BGV_FOLD_ARGS                                                                                         \
   const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const fp12_t *__restrict__ f,                     \
       const fp12_t *__restrict__ gpair, int32_t *__restrict__ verdict, fp12_t *__restrict__ gprod,          \
       fp12_t *__restrict__ gu, const fp12_t *__restrict__ gu1, const fp12_t *__restrict__ fsig
-__global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold(BGV_FOLD_ARGS) {
-  final_fold_body<true>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+__global__ void __launch_bounds__(BGV_FOLD_RNS_THREADS) k_final_fold(BGV_FOLD_ARGS) {
+  final_fold_body<2>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+}
+__global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold_p8(BGV_FOLD_ARGS) {
+  final_fold_body<1>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
 }
 __global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold_sel(BGV_FOLD_ARGS) {
-  final_fold_body<false>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+  final_fold_body<0>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
 }
 
 // Products of runs of Fp12 values (cross-process partials): team t of the
@@ -336,6 +371,10 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
     const char* e = getenv("BGV_FOLD_LEAN");
     return !(e && atoi(e) == 0);
   }();
+  static const bool rns = [] {
+    const char* e = getenv("BGV_FOLD_RNS");
+    return !(e && atoi(e) == 0);
+  }();
   if (b.weighted && !b.gu) return hipErrorInvalidValue;
   // A retry round of a uniform batch (b.uniform: tests inside uniform first-pass groups, whose
   // slots have no pair f_i of their own) closes on k_final12, which multiplies the tests' pubkey-
@@ -343,7 +382,8 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   // just above the latency bound on its first pass can fall below it here (advisor r05), and
   // k_final_fold would multiply the groups' unwritten f_i instead.
   if (!b.uniform && b.nslots + b.ngroups <= bgv_latency_max())
-    hipLaunchKernelGGL(lean ? k_final_fold : k_final_fold_sel, dim3(b.ngroups), dim3(BGV_FOLD_THREADS), 0, s.main, b.groups,
+    hipLaunchKernelGGL(rns ? k_final_fold : (lean ? k_final_fold_p8 : k_final_fold_sel), dim3(b.ngroups),
+                       dim3(rns ? BGV_FOLD_RNS_THREADS : BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,
                        !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
