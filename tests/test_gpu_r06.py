@@ -101,3 +101,25 @@ def test_uniform_group_values_pinned_to_oracle():
         e = expect(mask, weighted)
         assert o.final_exp(f12_from_bytes(pk576)) == e, (hex(mask), weighted, "pubkey-sum pair")
         assert o.final_exp(f12_from_bytes(sig576)) == o.f12_inv(e), (hex(mask), weighted, "signature pair")
+
+
+# ---------------------------------------------------------------------------------------
+# The residue-number-system Fp12 engine of k_final_fold (bgv_rns.h): its tm_pow_x chain, its
+# fp_t conversions in and out, and the eight-part engine it replaced, each checked against the
+# oracle on the same random Fp12 value (tools/gpu/rns_probe.py over tools/bin/ubench_rns, built
+# by __graft_entry__.build()); the probe also times both engines.
+# ---------------------------------------------------------------------------------------
+def test_rns_engine_probe():
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tools", "bin", "ubench_rns")
+    assert os.path.exists(exe), "tools/bin/ubench_rns missing: run __graft_entry__.build()"
+    res = subprocess.run([sys.executable, os.path.join(root, "tools", "gpu", "rns_probe.py"), "2", "11"],
+                         capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stdout + res.stderr
+    verdict = json.loads(res.stdout.strip().splitlines()[-1])
+    assert verdict["rns_chain_ok"] and verdict["rns_from_fp_ok"] and verdict["rns_to_fp_ok"] and verdict["part8_chain_ok"]
+    assert verdict["rns_output_bound_p"] < 16

@@ -316,6 +316,7 @@ def emit_header(path):
         f.write("#define BGV_RNS_BETA_SHIFT %d\n#define BGV_RNS_BETA_ROUND 0x%xull\n" % (BETA_SHIFT, BETA_ROUND))
         f.write(c_array("kRnsMod", mods))
         f.write(c_array("kRnsXi", xi))    # B: -p^-1 M_i^-1; B': M'_j^-1
+        f.write(c_array("kRnsXi2", [0 if i < NB else L[i]["minv"] * L[i]["xi"] % L[i]["m"] for i in range(30)]))  # B': M^-1 M'_j^-1
         f.write(c_array("kRnsAux", aux))  # B: -M' mod m_i; B': M^-1 mod m'_j
         f.write(c_array("kRnsPm", pm))    # p mod m
         f.write(c_array("kRnsKp", kp))    # K p mod m
