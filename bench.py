@@ -703,7 +703,7 @@ def node_shape(native, devices, nkeys, steps, warmup, settle_s, sweep=True):
 
 
 # PMC bytes per launch of the roofline call for the current kernels (tools/gpu/s3_pmc.sh)
-TRAFFIC_FILE = os.path.join("profiles", "r05", "traffic.json")
+TRAFFIC_FILE = os.path.join("profiles", "r06", "traffic.json")
 ROOF_SETS = 64512  # 63 x 1024: with its 1008 group lanes k_miller is one wave on each of the 1024 SIMDs
 
 
