@@ -402,10 +402,18 @@ BGV_NOINLINE fp_t fp_pow_fixed(const fp_t& a) {
     const uint32_t st = s.step[ku];
     const int d = (int)(st >> 8), nsq = (int)(st & 0xff);
     const fp_t m = tab[d & 15];
-#if defined(BGV_POW_INLINE)
-    // the chain's products inline (one copy each in the loop): no call per squaring
-    BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) r = fp_sqr_body(r);
-    if (d != 0xff) r = fp_mul_body(r, m);
+#if !defined(BGV_POW_CALLS)
+    // the chain's products inline (one copy each in the loop): no call per squaring.  Round 6:
+    // k_prep 12.46-12.48 vs 12.65-12.70 ms per 64,512-set launch, headline 2.655-2.663 vs
+    // 2.636-2.640 M sets/s interleaved (profiles/r06/ab_powinl/); BGV_POW_CALLS keeps the calls
+    BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) {
+      BGV_COUNT_SQR();
+      r = fp_sqr_body(r);
+    }
+    if (d != 0xff) {
+      BGV_COUNT_MUL();
+      r = fp_mul_body(r, m);
+    }
 #else
     BGV_NO_UNROLL for (int q = 0; q < nsq; ++q) r = fp_sqr(r);
     if (d != 0xff) r = fp_mul(r, m);
