@@ -429,6 +429,11 @@ struct PatternUnit {
 // units from the first pass of at most this many jobs (not pattern-testable) are tested one
 // job per device group
 static const size_t kSingletonMax = 8;
+// a signing root with at least this many one-set jobs starts its own device group (call_submit)
+#ifndef BGV_UNIFORM_ALIGN_MIN
+#define BGV_UNIFORM_ALIGN_MIN 32  // A/B: a huge value keeps the round-5 layout (roots back to back)
+#endif
+static const size_t kUniformAlignMin = BGV_UNIFORM_ALIGN_MIN;
 
 // One bgv_verify call travelling through a dispatcher.
 struct Call {
@@ -918,6 +923,7 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   // that the sets of a root fill whole groups (BGV_GROUP_UNIFORM: one Miller loop for the group;
   // gossip attestations of one committee share a root); then multi-set jobs.
   std::vector<size_t> shared_order;
+  std::vector<size_t> breaks;  // positions in shared_order where a new device group starts
   size_t n_one = 0;
   for (size_t j : call->todo)
     if (call->shared_job(j) && jobs[j].n_sets == 1) ++n_one;
@@ -948,7 +954,19 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
       buckets[b].push_back(j);
     }
     if (grouped) {
-      for (const auto& bk : buckets) shared_order.insert(shared_order.end(), bk.begin(), bk.end());
+      // A root with at least half a group of jobs starts a group of its own, so its groups stay
+      // uniform whatever the roots before it held (a committee one set short -- a corrupted
+      // message, a late attestation -- would otherwise shift every later root across a group
+      // boundary: both groups mixed, per-slot Miller loops, pattern tests instead of the weighted
+      // one); the roots with fewer jobs share mixed groups after them, in order of appearance.
+      for (const auto& bk : buckets)
+        if (bk.size() >= kUniformAlignMin) {
+          breaks.push_back(shared_order.size());
+          shared_order.insert(shared_order.end(), bk.begin(), bk.end());
+        }
+      breaks.push_back(shared_order.size());
+      for (const auto& bk : buckets)
+        if (bk.size() < kUniformAlignMin) shared_order.insert(shared_order.end(), bk.begin(), bk.end());
       for (size_t j : call->todo)
         if (call->shared_job(j) && jobs[j].n_sets != 1) shared_order.push_back(j);
     }
@@ -956,9 +974,14 @@ static int call_submit(bgv_ctx* c, Call* call, const bgv_job* jobs, size_t njobs
   if (shared_order.empty())  // call order
     for (size_t j : call->todo)
       if (call->shared_job(j)) shared_order.push_back(j);
-  for (size_t j : shared_order)
+  size_t bi = 0;
+  for (size_t q = 0; q < shared_order.size(); ++q) {
+    if (bi < breaks.size() && breaks[bi] == q) B.close_group();
+    while (bi < breaks.size() && breaks[bi] <= q) ++bi;
+    const size_t j = shared_order[q];
     for (uint32_t k = 0; k < jobs[j].n_sets; ++k)
       B.add((int)j, jobs[j].first_set + k, sets[jobs[j].first_set + k], k == 0);
+  }
   B.pad_to_wave();
   // A batchable job over several groups may be retried by fanout over its slots, which needs
   // their own pairs: its groups are not uniform.  A non-batchable job is never retried (its
@@ -1347,10 +1370,18 @@ static void call_after_round(Call* call, const int32_t* rv) {
       if (!cand.empty())
         for (size_t i = 0; i < n; ++i)
           if (std::find(cand.begin(), cand.end(), pu.jobs[i]) != cand.end()) idx.push_back((uint32_t)i);
+      // every index bit with both S_b and its complement failing (D covers all k bits: every
+      // job a candidate) means many invalid jobs (two have all their index bits apart with
+      // probability 1/(n-1)): the next round tests them one by one (no D: singles) instead of
+      // pairs whose failures would need a third round
+#ifndef BGV_RETRY_ALLBITS_SINGLES
+#define BGV_RETRY_ALLBITS_SINGLES 1  // A/B: 0 keeps the pairs round for every unit with a D
+#endif
+      const bool all_bits = BGV_RETRY_ALLBITS_SINGLES && k > 0 && D == (k >= 32 ? 0xffffffffu : ((1u << k) - 1u));
       call->units.push_back(cand.empty() ? pu.jobs : cand);
       call->unit_group.push_back((int)pu.group);
       call->unit_rounds.push_back(1);
-      call->unit_dmask.push_back(cand.empty() ? 0 : D);
+      call->unit_dmask.push_back(cand.empty() || all_bits ? 0 : D);
       call->unit_idx.push_back(std::move(idx));
     }
   }
