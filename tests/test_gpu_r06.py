@@ -123,3 +123,49 @@ def test_rns_engine_probe():
     verdict = json.loads(res.stdout.strip().splitlines()[-1])
     assert verdict["rns_chain_ok"] and verdict["rns_from_fp_ok"] and verdict["rns_to_fp_ok"] and verdict["part8_chain_ok"]
     assert verdict["rns_output_bound_p"] < 16
+
+
+# ---------------------------------------------------------------------------------------
+# Root-aligned layout (round 6, bgv_api.cpp call_submit): roots with >= 32 one-set jobs start
+# device groups of their own, the smaller roots share mixed groups after them; a pattern unit
+# whose every index bit failed both ways goes to singles.  Roots of 100, 40, 33, 32, 31, 5 and 1
+# jobs interleaved in call order, wrong keys inside the large roots, a mixed region whose jobs
+# are all invalid (every pattern bit fails), and a valid singleton: every verdict must equal the
+# job verified alone (multithread/worker.ts:76-98).
+# ---------------------------------------------------------------------------------------
+def test_root_aligned_layout_verdicts(ctx):
+    import random
+    from lodestar_amd import native
+    c, sks = ctx
+    rnd = random.Random(0xA11C)
+    sizes = [100, 40, 1, 33, 5, 32, 31, 1, 1, 100] + [1] * 40
+    roots, order = [], []
+    for r, n in enumerate(sizes):
+        roots.append(hashlib.sha256(b"r06-layout-%d" % r).digest())
+        order += [r] * n
+    rnd.shuffle(order)  # roots recur after one another: the grouped layout
+    n = len(order)
+    msgs = [roots[r] for r in order]
+    keys = [(i * 13) % NKEYS for i in range(n)]
+    sigs = c.sign(b"".join(sks[k] for k in keys), b"".join(msgs))
+    sets = [native.SetSpec(msgs[i], sigs[96 * i:96 * i + 96], pk_indices=[keys[i]]) for i in range(n)]
+    want = [1] * n
+    big = [i for i in range(n) if sizes[order[i]] >= 32]
+    for i in rnd.sample(big, 6):  # wrong keys inside the aligned roots
+        sets[i] = native.SetSpec(msgs[i], sets[i].sig, pk_indices=[(keys[i] + 1) % NKEYS])
+        want[i] = 0
+    small = [i for i in range(n) if sizes[order[i]] == 1]
+    for i in small[:-1]:  # the mixed region all invalid but one
+        sets[i] = native.SetSpec(msgs[i], sets[i].sig, pk_indices=[(keys[i] + 3) % NKEYS])
+        want[i] = 0
+    # pad the call past the bulk/uniform thresholds with valid distinct-root sets (call order)
+    extra = 16384  # bulk batch (nslots + ngroups > BGV_LATENCY_MAX): uniform groups and weighted tests
+    emsgs = [hashlib.sha256(b"r06-layout-extra-%d" % i).digest() for i in range(extra)]
+    ekeys = [(7 * i + 1) % NKEYS for i in range(extra)]
+    esigs = c.sign(b"".join(sks[k] for k in ekeys), b"".join(emsgs))
+    sets += [native.SetSpec(emsgs[i], esigs[96 * i:96 * i + 96], pk_indices=[ekeys[i]]) for i in range(extra)]
+    want += [1] * extra
+    jobs = [([s], True) for s in sets]
+    st = native.BgvStats()
+    assert c.verify_jobs(jobs, native.MODE_WORKER, stats=st) == want
+    assert st.batch_retries >= 1
