@@ -327,9 +327,73 @@ BGV_MILLER_ATTR auto lz_pline_add(lz_tpt& t, const lz2r& qx, const lz2r& qy, con
   return lz_pline_t<std::decay_t<decltype(L0)>, std::decay_t<decltype(L1)>, std::decay_t<decltype(L3)>>{L0, L1, L3};
 }
 
+// Round 6: the bulk walk (k_lines) in homogeneous projective coordinates, x = X/Z, y = Y/Z.
+// Doubling (a = 0, b' = 4(1 + i); Costello-Lange-Naehrig, all coordinates times 4): B = Y^2,
+// C = Z^2, E = 3 b' C, F = 3E, H = (Y + Z)^2 - B - C = 2YZ,
+//   X3 = 2XY (B - F), Y3 = (B + F)^2 - 12 E^2, Z3 = 4 B H,
+// and the tangent scaled by 2YZ: H yP - 3X^2 xP + (B - E), i.e. L0 = B - E, L1 = 3X^2, L3 = H in
+// the records' convention (l = L0 - L1 xP + L3 yP, scaled by P as before): 3 products + 6
+// squarings against the Jacobian step's 4 + 7.  Addition T + Q (Q projective; add-1998-cmo-2):
+// u = Y2 Z1 - Y1 Z2, v = X2 Z1 - X1 Z2, X3 = v A, Y3 = u (R - A) - v^3 Y1 Z2, Z3 = v^3 Z1 Z2
+// (R = v^2 X1 Z2, A = u^2 Z1 Z2 - v^3 - 2R), the chord through Q scaled by v Z2:
+// L0 = u X2 - v Y2, L1 = u Z2, L3 = v Z2.  Other representatives of the same lines (Fp2
+// factors the final exponentiation removes): the same pairing values as the Jacobian walk
+// (tests/test_pairing_golden.py, and on the device tests/test_gpu_pairing.py).
+BGV_MILLER_ATTR auto lz_pline_dbl_p(lz_tpt& t) {
+  const lz2r B = lz2_sqr(t.y);
+  const lz2r C = lz2_sqr(t.z);
+  const lz2r XX = lz2_sqr(t.x);
+  const lz2r E = lz2_red(lz2_mulk<12>(lz2_norm(lz2_mul_xi(C))));  // 3 b' C = 12 (1 + i) C
+  const auto F = lz2_mulk<3>(E);
+  const auto H = lz2_norm(lz2_sub(lz2_sqr(lz2_norm(lz2_add(t.y, t.z))), lz2_add(B, C)));
+  const auto XY = lz2_mul(t.x, t.y);
+  const auto X3 = lz2_mul(lz2_wnorm(lz2_dbl(XY)), lz2_wnorm(lz2_norm(lz2_sub(B, F))));
+  const auto Y3 = lz2_sub(lz2_sqr(lz2_norm(lz2_add(B, F))), lz2_mulk<12>(lz2_sqr(E)));
+  const auto Z3 = lz2_mulk<4>(lz2_mul(B, H));
+  const auto L0 = lz2_norm(lz2_sub(B, E));
+  const auto L1 = lz2_norm(lz2_mulk<3>(XX));
+  const auto L3 = H;
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+  return lz_pline_t<std::decay_t<decltype(L0)>, std::decay_t<decltype(L1)>, std::decay_t<decltype(L3)>>{L0, L1, L3};
+}
+BGV_MILLER_ATTR auto lz_pline_add_p(lz_tpt& t, const lz2r& qx, const lz2r& qy, const lz2r& qz) {
+  const auto Y1Z2 = lz2_mul(t.y, qz);
+  const auto X1Z2 = lz2_mul(t.x, qz);
+  const auto Z1Z2 = lz2_mul(t.z, qz);
+  const auto u = lz2_norm(lz2_sub(lz2_mul(qy, t.z), Y1Z2));
+  const auto v = lz2_norm(lz2_sub(lz2_mul(qx, t.z), X1Z2));
+  const lz2r uu = lz2_sqr(u);
+  const lz2r vv = lz2_sqr(v);
+  const auto vvv = lz2_mul(v, vv);
+  const auto R = lz2_mul(vv, X1Z2);
+  const auto A = lz2_norm(lz2_sub(lz2_mul(uu, Z1Z2), lz2_add(vvv, lz2_dbl(R))));
+  const auto X3 = lz2_mul(v, A);
+  const auto Y3 = lz2_sub(lz2_mul(u, lz2_wnorm(lz2_norm(lz2_sub(R, A)))), lz2_mul(vvv, Y1Z2));
+  const auto Z3 = lz2_mul(vvv, Z1Z2);
+  const auto L0 = lz2_norm(lz2_sub(lz2_mul(u, qx), lz2_mul(v, qy)));
+  const auto L1 = lz2_norm(lz2_mul(u, qz));
+  const auto L3 = lz2_norm(lz2_mul(v, qz));
+  t.x = lz2_red(X3);
+  t.y = lz2_red(Y3);
+  t.z = lz2_red(Z3);
+  return lz_pline_t<std::decay_t<decltype(L0)>, std::decay_t<decltype(L1)>, std::decay_t<decltype(L3)>>{L0, L1, L3};
+}
+// Jacobian Q (x = X/Z^2, y = Y/Z^3) as projective: (X Z, Y, Z^3)
+BGV_HD lz_tpt lz_tpt_proj(const g2_jac& q) {
+  const lz2r z = lz2_in(q.z);
+  return lz_tpt{lz2_red(lz2_mul(lz2_in(q.x), z)), lz2_in(q.y), lz2_red(lz2_mul(lz2_sqr(z), z))};
+}
+
 // the record types the two phases agree on
+#if defined(BGV_LINES_JACOBIAN)  // A/B: round 5's Jacobian walk
 typedef decltype(lz_pline_dbl(*(lz_tpt*)nullptr)) lz_pline_d;
 typedef decltype(lz_pline_add(*(lz_tpt*)nullptr, lz2r{}, lz2r{}, lz2r{})) lz_pline_a;
+#else
+typedef decltype(lz_pline_dbl_p(*(lz_tpt*)nullptr)) lz_pline_d;
+typedef decltype(lz_pline_add_p(*(lz_tpt*)nullptr, lz2r{}, lz2r{}, lz2r{})) lz_pline_a;
+#endif
 
 // the line of a record scaled by P (6 products), as an Fp12 factor's three coefficients
 template <class Lp>
@@ -395,6 +459,7 @@ BGV_HD bool miller_add_at(int i) { return (BGV_X_ABS >> (i + 1)) & 1; }
 // the loads), so the 63 doublings keep only T and their temporaries live.
 template <class Emit>
 BGV_HD void miller_lines_walk(const g2_jac* qm, Emit emit) {
+#if defined(BGV_LINES_JACOBIAN)
   lz_tpt t = {lz2_in(qm[0].x), lz2_in(qm[0].y), lz2_in(qm[0].z)};
   int k = 0;
   emit(k++, lz_pline_dbl(t));
@@ -405,6 +470,18 @@ BGV_HD void miller_lines_walk(const g2_jac* qm, Emit emit) {
     }
     emit(k++, lz_pline_dbl(t));
   }
+#else
+  lz_tpt t = lz_tpt_proj(qm[0]);
+  int k = 0;
+  emit(k++, lz_pline_dbl_p(t));
+  BGV_NO_UNROLL for (int i = 61; i >= 0; --i) {
+    if (miller_add_at(i)) {
+      const lz_tpt q = lz_tpt_proj(qm[bgv_opaque0()]);  // Q again from memory: not live across the doublings
+      emit(k++, lz_pline_add_p(t, q.x, q.y, q.z));
+    }
+    emit(k++, lz_pline_dbl_p(t));
+  }
+#endif
 }
 
 // k_facc's walk with the records and P's constants in LDS: load(k, rec) fills record k,
