@@ -198,7 +198,7 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
                                                 const fp12_t* __restrict__ f, const fp12_t* __restrict__ gpair,
                                                 int32_t* __restrict__ verdict, fp12_t* __restrict__ gprod,
                                                 fp12_t* __restrict__ gu, const fp12_t* __restrict__ gu1,
-                                                const fp12_t* __restrict__ fsig) {
+                                                const fp12_t* __restrict__ fsig, const fp12_t* __restrict__ gpkp) {
   constexpr int kTeams = (ENGINE == 2 ? BGV_FOLD_RNS_THREADS : BGV_FOLD_THREADS) / BGV_TEAM;
   __shared__ fp_t lds[kTeams][2 * BGV_TEAM_COMPS];
   __shared__ fp_t part[BGV_FOLD_TEAMS][BGV_TEAM_COMPS];
@@ -216,7 +216,10 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
   // the group's signature pair, or (fsig: bgv_sig_pairs) each slot's own
   fp_t x = team == 0 && !fsig ? reinterpret_cast<const fp_t*>(gpair + (gi < ngroups ? gi : ngroups - 1))[fi] : one_c;
   const fp_t* ss = fsig ? reinterpret_cast<const fp_t*>(fsig + g.first_slot) : nullptr;
-  const uint32_t nmax = (g.n_slots + BGV_FOLD_TEAMS - 1) / BGV_FOLD_TEAMS;
+  // gpkp (retry rounds of uniform batches, as k_final12): a uniform test multiplies its one
+  // pubkey-sum pair instead of its slots' pairs (uniform over the block)
+  const bool uni = gpkp && gi < ngroups && (g.flags & BGV_GROUP_UNIFORM);
+  const uint32_t nmax = uni ? 0u : (g.n_slots + BGV_FOLD_TEAMS - 1) / BGV_FOLD_TEAMS;
   BGV_NO_UNROLL for (uint32_t k = 0; k < nmax; ++k) {
     const uint32_t idx = team + BGV_FOLD_TEAMS * k;
     const bool in = fold && grp_has(g, idx);
@@ -232,6 +235,7 @@ __device__ __forceinline__ void final_fold_body(const bgv_dgroup* __restrict__ g
     const int t2 = 2 * (team % (w >> 1));
     x = o.mul(part[t2][cc], part[t2 + 1][cc]);
   }
+  if (gpkp) x = o.mul(x, uni && team == 0 ? reinterpret_cast<const fp_t*>(gpkp + gi)[fi] : one_c);  // grid-uniform
   if (gprod && gi < ngroups && team == 0 && c < BGV_TEAM_COMPS) reinterpret_cast<fp_t*>(gprod + gi)[fi] = x;
   // the final exponentiation on the whole block with the wide products (bgv_team_dev.h)
   if (team == 0 && c < BGV_TEAM_COMPS) W[cc] = x;
@@ -276,15 +280,16 @@ extern "C" {
 #define BGV_FOLD_ARGS                                                                                         \
   const bgv_dgroup *__restrict__ groups, uint32_t ngroups, const fp12_t *__restrict__ f,                     \
       const fp12_t *__restrict__ gpair, int32_t *__restrict__ verdict, fp12_t *__restrict__ gprod,          \
-      fp12_t *__restrict__ gu, const fp12_t *__restrict__ gu1, const fp12_t *__restrict__ fsig
+      fp12_t *__restrict__ gu, const fp12_t *__restrict__ gu1, const fp12_t *__restrict__ fsig,                \
+      const fp12_t *__restrict__ gpkp
 __global__ void __launch_bounds__(BGV_FOLD_RNS_THREADS) k_final_fold(BGV_FOLD_ARGS) {
-  final_fold_body<2>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+  final_fold_body<2>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig, gpkp);
 }
 __global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold_p8(BGV_FOLD_ARGS) {
-  final_fold_body<1>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+  final_fold_body<1>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig, gpkp);
 }
 __global__ void __launch_bounds__(BGV_FOLD_THREADS) k_final_fold_sel(BGV_FOLD_ARGS) {
-  final_fold_body<0>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig);
+  final_fold_body<0>(groups, ngroups, f, gpair, verdict, gprod, gu, gu1, fsig, gpkp);
 }
 
 // Products of runs of Fp12 values (cross-process partials): team t of the
@@ -359,6 +364,9 @@ __global__ void k_fp12_from_bytes(const uint8_t* __restrict__ in, uint32_t n, fp
 // bgv_launch_miller (first pass, group pairs already made) or, for a retry round over the
 // same per-slot results, with pairs = true: the parts' signature sums and pairs first.
 uint32_t bgv_fold_pairs_max() { return bgv_latency_max(); }
+#ifndef BGV_RETRY_FOLD_MAX
+#define BGV_RETRY_FOLD_MAX 512
+#endif
 
 hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool pairs) {
   if (b.ngroups == 0) return hipSuccess;
@@ -381,12 +389,25 @@ hipError_t bgv_launch_groups(const bgv_dev_batch& b, const bgv_streams& s, bool 
   // sum pairs (gpkp), whatever its size: its b.ngroups counts only the round's tests, so a batch
   // just above the latency bound on its first pass can fall below it here (advisor r05), and
   // k_final_fold would multiply the groups' unwritten f_i instead.
-  if (!b.uniform && b.nslots + b.ngroups <= bgv_latency_max())
+  // A retry round of a uniform batch with at most BGV_RETRY_FOLD_MAX tests (env; 0: none)
+  // closes on k_final_fold whatever the batch's size: one block per test, its final
+  // exponentiation in residue arithmetic (~0.55 against ~2.8 ms for k_final12's teams) at ~6x
+  // the SIMD time per test.  Mainnet-shaped windows (uniform batches, their rate bound by the
+  // retry thread's round latency): 5.05-5.17 against 4.47-4.81 M sets/s; on the headline's
+  // non-uniform batches it cost 0.4 % (512 tests) to 30 % (every round), so those stay on
+  // k_final12 (profiles/r06/retry_fold/).
+  static const uint32_t retry_fold_max = [] {
+    const char* e = getenv("BGV_RETRY_FOLD_MAX");
+    return e ? (uint32_t)atoi(e) : (uint32_t)BGV_RETRY_FOLD_MAX;
+  }();
+  const bool small_retry = pairs && b.uniform && b.ngroups <= retry_fold_max;
+  if ((!b.uniform && b.nslots + b.ngroups <= bgv_latency_max()) || small_retry)
     hipLaunchKernelGGL(rns ? k_final_fold : (lean ? k_final_fold_p8 : k_final_fold_sel), dim3(b.ngroups),
                        dim3(rns ? BGV_FOLD_RNS_THREADS : BGV_FOLD_THREADS), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair,
                        b.verdict, b.gprod, b.gu, b.gu1,
-                       !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr);
+                       !pairs && bgv_sig_pairs(b) ? static_cast<const fp12_t*>(b.fsig) : nullptr,
+                       b.uniform ? static_cast<const fp12_t*>(b.gpkp) : nullptr);
   else
     hipLaunchKernelGGL(k_final12, dim3(nblk(b.ngroups, BGV_FINAL12_TEAMS)), dim3(64), 0, s.main, b.groups,
                        b.ngroups, b.f, b.gpair, b.verdict, b.gprod, b.gu, b.gu1,
