@@ -1,5 +1,6 @@
 # Config-3 latency with the previous library (idle window for every call) against the current
 # one (no idle window for calls without batchable jobs), interleaved; then the GPU suite.
+# (The change was reverted after this run; lodestar_amd/ab_prev/ held the previous build for it: profiles/r06/idle_window/)
 set -o pipefail; O=${1:-gpurun_out/r06idle}; mkdir -p $O; export TMPDIR=/tmp
 for i in 1 2 3; do
   BLSGPU_LIB=$PWD/lodestar_amd/ab_prev/libblsgpu.so timeout -k 10 200 python tools/gpu/latency_probe.py 60 >> $O/config3_prev.jsonl 2>> $O/err.txt || exit 1
